@@ -1,0 +1,216 @@
+"""bench.py — session-frames resimulated per second at an 8-frame rollback.
+
+Workload (BASELINE.json configs[1]): 65,536 independent ex_game SyncTest
+sessions per GPU, 2 players, check_distance 7 (max_prediction 8), input
+delay 2: every step (= one tick) loads frame c-7, resimulates and re-saves 7
+frames, saves frame c and advances to c+1 — 8 AdvanceFrames per session.
+Synthetic seeded inputs (ggrs_amd.synth), resident in HBM before timing.
+
+N>1: one process per GPU (torch.distributed.run), sessions sharded (weak
+scaling: sessions per GPU fixed), no data-path collective; every
+--report-interval ticks the per-session desync reports (checksum of the last
+settled frame + mismatch flag) are all-gathered over RCCL.
+
+Prints ONE JSON line (rank 0).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "session-frames resimulated/sec (node) at 8-frame rollback; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def algorithmic_bytes_per_session_tick(P: int, cd: int, nw: int, cs_bytes: int, in_rec: int, in_bytes: int) -> int:
+    """Bytes one steady-state tick must move per session:
+    1 snapshot load + cd snapshot saves, cd cell checksums written, cd-1
+    first-seen reads + 1 first-seen write, cd+1 input records read, the new
+    inputs read and written to the input ring, the display checksum written."""
+    state = 4 * nw
+    return (state * (1 + cd) + cs_bytes * cd + cs_bytes * (cd - 1) + cs_bytes + in_rec * (cd + 1)
+            + P * in_bytes + in_rec + cs_bytes)
+
+
+def cpu_baseline(args, P):
+    from oracle import oracle as O
+    threads = max(1, min(16, os.cpu_count() or 1))
+    S, warm, ticks = args.cpu_sessions, 16, args.cpu_ticks
+    secs, nerr = O.bench_exgame(P, args.check_distance, args.input_delay, args.max_prediction, S, warm, ticks,
+                                threads, args.seed)
+    sf = S * ticks * (args.check_distance + 1)
+    return {"value": sf / secs, "unit": "session-frames/s", "cores": threads, "kind": "port",
+            "sample": f"{S} ex_game sessions x {ticks} steady-state ticks ({sf} session-frames) of the C++ "
+                      f"line-faithful restatement (reference allocation pattern), {threads} host threads, "
+                      f"{secs:.2f} s wall, {nerr} errors"}
+
+
+def pmc_traffic(cfg_key):
+    """HBM bytes per tick launch from the committed rocprofv3 PMC summary of this
+    exact configuration (profiles/*pmc*.json, written by tools/pmc_summary.py), or None."""
+    import glob
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+        try:
+            d = json.load(open(path))
+        except Exception:
+            continue
+        if d.get("config_key") == cfg_key and d.get("hbm_bytes_per_launch"):
+            best = d["hbm_bytes_per_launch"]
+    return best
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--warmup", type=int, default=32)
+    ap.add_argument("--sessions-per-gpu", type=int, default=65536)
+    ap.add_argument("--num-players", type=int, default=2)
+    ap.add_argument("--check-distance", type=int, default=7)
+    ap.add_argument("--max-prediction", type=int, default=8)
+    ap.add_argument("--input-delay", type=int, default=2)
+    ap.add_argument("--seed", type=int, default=0x67677273)
+    ap.add_argument("--report-interval", type=int, default=100,
+                    help="ticks between RCCL all-gathers of desync reports (N>1); 0 = never")
+    ap.add_argument("--cpu-sessions", type=int, default=16384)
+    ap.add_argument("--cpu-ticks", type=int, default=32)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--block-size", type=int, default=0)
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import ggrs_amd as G
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
+
+    P, cd = args.num_players, args.check_distance
+    S = args.sessions_per_gpu
+    T = args.warmup + args.steps
+    # This rank's shard: global sessions [rank*S, (rank+1)*S); inputs keyed by global id.
+    inputs = G.synth_inputs(S * world, P, T, seed=args.seed)[:, :, rank * S:(rank + 1) * S]
+    dinputs = torch.from_numpy(np.ascontiguousarray(inputs)).to(dev)  # [T, P, S] u8, resident in HBM
+
+    stream = torch.cuda.Stream(device=dev)
+    sess = (G.SessionBuilder(G.Game.EX_GAME, num_sessions=S, device=local).with_num_players(P)
+            .with_max_prediction_window(args.max_prediction).with_check_distance(cd)
+            .with_input_delay(args.input_delay).with_checked_mismatches(False)
+            .with_block_size(args.block_size).start_synctest_session())
+    sess.set_stream(stream)
+    reports = torch.zeros((S, 3), dtype=torch.int64, device=dev)  # rb_checksum_report, 24 B
+    gathered = torch.zeros((S * world, 3), dtype=torch.int64, device=dev) if world > 1 else None
+    desyncs = torch.zeros((), dtype=torch.int64, device=dev)
+
+    def tick(t):
+        for h in range(P):
+            sess.add_local_input(h, dinputs[t, h])
+        sess.advance_frame()
+        if world > 1 and args.report_interval and sess.current_frame() % args.report_interval == 0:
+            f = sess.current_frame() - 1
+            sess.export_checksum_report(f, reports.data_ptr())
+            dist.all_gather_into_tensor(gathered, reports)  # RCCL allgather of desync reports
+            desyncs.add_(((gathered[:, 2] >> 32) != -1).sum())  # mismatch_frame != NULL_FRAME
+
+    with torch.cuda.stream(stream):
+        for t in range(args.warmup):
+            tick(t)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        sess.profile_enable(True)
+        sess.profile_take()
+        t0 = time.perf_counter()
+        for t in range(args.warmup, T):
+            tick(t)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        kernel_ms, launches = sess.profile_take()
+
+    nfail = int((sess.mismatches() != G.NULL_FRAME).sum())
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    bad = torch.tensor([nfail + int(desyncs.item())], dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dist.all_reduce(bad, op=dist.ReduceOp.SUM)
+    elapsed = float(el.item())
+
+    if rank == 0:
+        frames_per_tick = cd + 1
+        total = S * world * frames_per_tick * args.steps
+        value = total / elapsed
+        avg_kernel_s = kernel_ms / 1e3 / max(1, launches)
+        bpt = algorithmic_bytes_per_session_tick(P, cd, nw=5 * P, cs_bytes=2, in_rec=2 if P == 2 else (1 if P == 1 else 4),
+                                                 in_bytes=1)
+        bytes_per_launch = bpt * S
+        achieved = bytes_per_launch / avg_kernel_s / 1e9
+        cfg_key = f"ex_game P={P} cd={cd} W={args.max_prediction} d={args.input_delay} S={S}"
+        traffic = pmc_traffic(cfg_key)
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "session-frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {
+                "workload": f"ex_game SyncTestSession x {S} sessions/GPU ({S * world} total), 2 players, "
+                            f"check_distance {cd} (8-frame rollback), input delay {args.input_delay}",
+                "sessions_per_gpu": S,
+                "total_sessions": S * world,
+                "num_players": P,
+                "max_prediction": args.max_prediction,
+                "check_distance": cd,
+                "input_delay": args.input_delay,
+                "session_frames_per_step_per_session": frames_per_tick,
+                "parallelism": f"session-sharded x{world}" + (f", RCCL allgather of desync reports every "
+                                                              f"{args.report_interval} ticks" if world > 1 else ""),
+                "mismatched_sessions": int(bad.item()),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": bytes_per_launch,
+                "kernel_avg_us": avg_kernel_s * 1e6,
+                "kernel": "tick_kernel<ExGame<2>>",
+            },
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args, P)
+        print(json.dumps(line), flush=True)
+    sess.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

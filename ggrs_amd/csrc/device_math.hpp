@@ -1,0 +1,171 @@
+// ggrs_amd/csrc/device_math.hpp — scalar arithmetic the game handlers need,
+// written so the GPU reproduces the reference's CPU results bit for bit.
+//
+// * sincosf_glibc: Rust's f32::sin/cos (ex_game.rs:282-288) lower to glibc's
+//   sinf/cosf on x86_64 Linux.  glibc 2.28+ evaluates them in double precision
+//   (sysdeps/ieee754/flt-32/s_sinf.c, s_cosf.c, sincosf.h, sincosf_data.c:
+//   reduce_fast + degree-4/5 polynomials).  That algorithm is restated here in
+//   double arithmetic, which the GPU executes with IEEE-exact add/mul/fma, so
+//   device results equal glibc's.  Checked exhaustively against the host libm
+//   for every float in [-0.1, 6.4] (tests/test_device_math.py, GPU) and on the
+//   host for all 2.1e9 floats of that range when this file was written.
+//   Only |x| < 120 is restated (ex_game rotations live in [0, 2*pi]); larger
+//   arguments fall back to the ocml routines and are counted as unexpected.
+// * fletcher16 closed form: the serial mod-255 loop of ex_game.rs:42-52 equals
+//   s1 = sum(b_i) mod 255, s2 = sum((n - i) * b_i) mod 255 (s2 sums every
+//   prefix s1).  Per 32-bit word that is two v_dot4_u32_u8.
+// * SipHash-1-3 with keys (0,0): Rust std DefaultHasher (tests/stubs.rs:8-12).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rb {
+
+// ----------------------------------------------------------------------------
+// glibc sinf/cosf restated (double evaluation, FMA form — the variant the
+// x86_64 ifunc selects on FMA-capable hosts; the non-FMA form gives identical
+// float results on this range, verified).
+// ----------------------------------------------------------------------------
+struct SinCos {
+  float s, c;
+};
+
+__device__ __forceinline__ uint32_t abstop12(float x) { return (__float_as_uint(x) >> 20) & 0x7ff; }
+
+// sincosf.h sinf_poly(x, x2, p, n) for n even (sine polynomial); s1..s3 are the
+// same in both __sincosf_table rows.
+__device__ __forceinline__ double sin_poly(double x, double x2) {
+  const double s1 = -0x1.555545995a603p-3, s2 = 0x1.1107605230bc4p-7, s3 = -0x1.994eb3774cf24p-13;
+  double x3 = x * x2;
+  double sp = __builtin_fma(x2, s3, s2);
+  double x7 = x3 * x2;
+  double s = __builtin_fma(x3, s1, x);
+  return __builtin_fma(x7, sp, s);
+}
+// sinf_poly for n odd (cosine polynomial) with __sincosf_table[0]; row [1] has
+// every c_i negated, which negates the result exactly.
+__device__ __forceinline__ double cos_poly(double x2) {
+  const double c0 = 0x1p0, c1 = -0x1.ffffffd0c621cp-2, c2 = 0x1.55553e1068f19p-5,
+               c3 = -0x1.6c087e89a359dp-10, c4 = 0x1.99343027bf8c3p-16;
+  double x4 = x2 * x2;
+  double cp2 = __builtin_fma(x2, c4, c3);
+  double cp1 = __builtin_fma(x2, c1, c0);
+  double x6 = x4 * x2;
+  double c = __builtin_fma(x4, c2, cp1);
+  return __builtin_fma(x6, cp2, c);
+}
+
+__device__ __forceinline__ SinCos sincosf_glibc(float y, uint32_t* unexpected) {
+  const float pio4 = 0x1.921FB6p-1f;
+  double x = y;
+  SinCos r;
+  if (abstop12(y) < abstop12(pio4)) {
+    if (abstop12(y) < abstop12(0x1p-12f)) {
+      r.s = y;
+      r.c = 1.0f;
+      return r;
+    }
+    double x2 = x * x;
+    r.s = static_cast<float>(sin_poly(x, x2));
+    r.c = static_cast<float>(cos_poly(x2));
+    return r;
+  }
+  if (abstop12(y) < abstop12(120.0f)) {
+    // reduce_fast, !TOINT_INTRINSICS form (x86_64): hpi_inv prescaled by 2^24.
+    const double hpi_inv = 0x1.45F306DC9C883p+23, hpi = 0x1.921FB54442D18p0;
+    double rr = x * hpi_inv;
+    int n = (static_cast<int32_t>(rr) + 0x800000) >> 24;
+    double xr = __builtin_fma(-static_cast<double>(n), hpi, x);
+    double sgn = ((n & 3) == 1 || (n & 3) == 2) ? -1.0 : 1.0;  // sign[4] = {1,-1,-1,1}
+    double xs = xr * sgn;
+    double x2 = xr * xr;
+    double sp = sin_poly(xs, x2);
+    double cp = cos_poly(x2);
+    if (n & 2) cp = -cp;  // __sincosf_table[1]
+    // sinf: n even -> sine poly, odd -> cosine poly; cosf uses n ^ 1.
+    r.s = static_cast<float>((n & 1) ? cp : sp);
+    r.c = static_cast<float>((n & 1) ? sp : cp);
+    return r;
+  }
+  if (unexpected) atomicAdd(unexpected, 1u);
+  r.s = sinf(y);
+  r.c = cosf(y);
+  return r;
+}
+
+// f32::rem_euclid (r = x % rhs; r < 0 ? r + |rhs| : r).  fmod is exact; for
+// |x| < 2|rhs| it is x or x -/+ rhs (Sterbenz), else the library fmodf.
+__device__ __forceinline__ float rem_euclid(float x, float rhs) {
+  float ay = __builtin_fabsf(rhs), ax = __builtin_fabsf(x);
+  float r;
+  if (ax < ay) {
+    r = x;
+  } else if (ax < 2.0f * ay) {
+    r = __builtin_copysignf(ax - ay, x);
+  } else {
+    r = fmodf(x, rhs);
+  }
+  return r < 0.0f ? r + ay : r;
+}
+
+// ----------------------------------------------------------------------------
+// fletcher16 closed form pieces
+// ----------------------------------------------------------------------------
+struct Fl16 {
+  uint32_t s1, s2;  // plain sums, reduced once at the end
+};
+// Add a 32-bit little-endian word whose first byte sits at image offset `o`
+// of an n-byte image: weights n-o, n-o-1, n-o-2, n-o-3 (all < 256 for the
+// images used here).
+__device__ __forceinline__ void fl16_word(Fl16& a, uint32_t w, uint32_t wpack) {
+  a.s1 = __builtin_amdgcn_udot4(w, 0x01010101u, a.s1, false);
+  a.s2 = __builtin_amdgcn_udot4(w, wpack, a.s2, false);
+}
+__host__ __device__ constexpr uint32_t fl16_weights(int n, int o) {
+  return static_cast<uint32_t>(n - o) | (static_cast<uint32_t>(n - o - 1) << 8) |
+         (static_cast<uint32_t>(n - o - 2) << 16) | (static_cast<uint32_t>(n - o - 3) << 24);
+}
+__device__ __forceinline__ uint16_t fl16_finish(const Fl16& a) {
+  return static_cast<uint16_t>(((a.s2 % 255u) << 8) | (a.s1 % 255u));
+}
+
+// ----------------------------------------------------------------------------
+// SipHash-1-3, keys (0,0), 8-byte message le32(a) || le32(b)
+// ----------------------------------------------------------------------------
+__host__ __device__ __forceinline__ uint64_t rotl64(uint64_t x, int b) { return (x << b) | (x >> (64 - b)); }
+#define RB_SIPROUND                                                      \
+  do {                                                                   \
+    v0 += v1; v1 = rotl64(v1, 13); v1 ^= v0; v0 = rotl64(v0, 32);        \
+    v2 += v3; v3 = rotl64(v3, 16); v3 ^= v2;                             \
+    v0 += v3; v3 = rotl64(v3, 21); v3 ^= v0;                             \
+    v2 += v1; v1 = rotl64(v1, 17); v1 ^= v2; v2 = rotl64(v2, 32);        \
+  } while (0)
+__host__ __device__ __forceinline__ uint64_t siphash13_i32x2(int32_t a, int32_t b) {
+  uint64_t v0 = 0x736f6d6570736575ULL, v1 = 0x646f72616e646f6dULL;
+  uint64_t v2 = 0x6c7967656e657261ULL, v3 = 0x7465646279746573ULL;
+  const uint64_t m = static_cast<uint64_t>(static_cast<uint32_t>(a)) |
+                     (static_cast<uint64_t>(static_cast<uint32_t>(b)) << 32);
+  v3 ^= m;
+  RB_SIPROUND;
+  v0 ^= m;
+  const uint64_t t = 8ULL << 56;  // length byte, empty tail
+  v3 ^= t;
+  RB_SIPROUND;
+  v0 ^= t;
+  v2 ^= 0xff;
+  RB_SIPROUND;
+  RB_SIPROUND;
+  RB_SIPROUND;
+  return v0 ^ v1 ^ v2 ^ v3;
+}
+#undef RB_SIPROUND
+
+__host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9e3779b97f4a7c15ULL;
+  x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  x = (x ^ (x >> 27)) * 0x94d049bb133111ebULL;
+  return x ^ (x >> 31);
+}
+
+}  // namespace rb

@@ -1,0 +1,826 @@
+// ggrs_amd/csrc/engine.hip — MI355X batched rollback-resimulation engine.
+//
+// One rb_batch = S independent SyncTestSessions in lock-step.  Per tick the
+// host mirror (planner.hpp) produces the reference's request stream and lowers
+// it to a TickProgram; ONE kernel launch then executes that stream for every
+// session: lane s owns session s, its state stays in VGPRs from the
+// LoadGameState through every SaveGameState/AdvanceFrame of the tick, and
+// HBM sees each snapshot written once (coalesced SoA planes) and the loaded
+// slot read once.
+//
+// Device layout (Spad = S rounded up to 64; all planes contiguous over sessions):
+//   snap  [W slots][NW words as planes of u32x4 / u32x2 / u32][Spad]   snapshot ring, slot = frame % W
+//   cs    [W][Spad] CS        checksum stored by each SaveGameState (GameStateCell::checksum)
+//   fs    [W][Spad] CS        first-seen checksum of the frame (SyncTestSession::checksum_history)
+//   ring  [128][Spad] InRec   confirmed inputs, slot = frame % 128 (InputQueue::inputs)
+//   live  [NW planes][Spad]   live game state between ticks when no LoadGameState follows
+//   err   [Spad] i32          MismatchedChecksum{frame}, NULL_FRAME when healthy
+//   frozen[Spad/64] u64       sessions whose advance_frame returns Err (they no longer advance)
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/ggrs_amd.h"
+#include "games.hpp"
+#include "planner.hpp"
+
+namespace rb {
+
+constexpr int kChunk = 8;  // inputs prefetched per chunk of AdvanceFrames
+constexpr int kMaxRepl = 8;
+
+struct KParams {
+  uint32_t* snap;
+  uint32_t* live;
+  void* cs;
+  void* fs;
+  void* ring;
+  void* last_cs;
+  void* periodic_cs;
+  int32_t* err;
+  unsigned long long* frozen;
+  uint32_t* counters;  // [0] sessions failed, [1] unexpected-path count
+  const void* in_ptr[4];
+  int32_t in_mode;  // 0: no new input, 1: one array per player, 2: packed [S][P]
+  int32_t S, Spad, W;
+  int32_t user_slot, n_repl, repl_src;
+  int32_t repl_dst[kMaxRepl];
+  int32_t load_slot;  // -1: start from the live state
+  int32_t f0, n_steps;
+  uint32_t save_modes[kMaxSteps / 16];  // 2 bits per step
+  int32_t live_out, periodic_step, display;
+  uint32_t disc_mask;
+  uint64_t seed;
+  uint32_t nonce_base;
+};
+
+// ---- SoA planes: word k of session s inside a block of NW planes -------------
+template <int NW>
+__device__ __forceinline__ void load_words(const uint32_t* __restrict__ base, int Spad, int s, uint32_t (&w)[NW]) {
+  constexpr int Q4 = NW / 4, R = NW % 4;
+#pragma unroll
+  for (int j = 0; j < Q4; ++j) {
+    const uint4 v = reinterpret_cast<const uint4*>(base + j * 4 * Spad)[s];
+    w[4 * j + 0] = v.x;
+    w[4 * j + 1] = v.y;
+    w[4 * j + 2] = v.z;
+    w[4 * j + 3] = v.w;
+  }
+  const uint32_t* b = base + Q4 * 4 * Spad;
+  if constexpr (R >= 2) {
+    const uint2 v = reinterpret_cast<const uint2*>(b)[s];
+    w[Q4 * 4 + 0] = v.x;
+    w[Q4 * 4 + 1] = v.y;
+    b += 2 * Spad;
+  }
+  if constexpr (R & 1) w[NW - 1] = b[s];
+}
+template <int NW>
+__device__ __forceinline__ void store_words(uint32_t* __restrict__ base, int Spad, int s, const uint32_t (&w)[NW]) {
+  constexpr int Q4 = NW / 4, R = NW % 4;
+#pragma unroll
+  for (int j = 0; j < Q4; ++j)
+    reinterpret_cast<uint4*>(base + j * 4 * Spad)[s] = make_uint4(w[4 * j], w[4 * j + 1], w[4 * j + 2], w[4 * j + 3]);
+  uint32_t* b = base + Q4 * 4 * Spad;
+  if constexpr (R >= 2) {
+    reinterpret_cast<uint2*>(b)[s] = make_uint2(w[Q4 * 4], w[Q4 * 4 + 1]);
+    b += 2 * Spad;
+  }
+  if constexpr (R & 1) b[s] = w[NW - 1];
+}
+// host mirror of the plane layout
+inline size_t word_index(int NW, int Spad, int s, int k) {
+  const int Q4 = NW / 4, R = NW % 4;
+  if (k < Q4 * 4) return static_cast<size_t>(k / 4) * 4 * Spad + static_cast<size_t>(s) * 4 + (k % 4);
+  size_t b = static_cast<size_t>(Q4) * 4 * Spad;
+  if (R >= 2) {
+    if (k < Q4 * 4 + 2) return b + static_cast<size_t>(s) * 2 + (k - Q4 * 4);
+    b += 2 * static_cast<size_t>(Spad);
+  }
+  return b + s;
+}
+
+template <class G>
+__device__ __forceinline__ typename G::InRec gather_new_input(const KParams& p, int s) {
+  using InRec = typename G::InRec;
+  constexpr int P = G::kPlayers, IB = G::kInputBytes;
+  if (p.in_mode == 2 && sizeof(InRec) == P * IB) return reinterpret_cast<const InRec*>(p.in_ptr[0])[s];
+  uint64_t v = 0;
+#pragma unroll
+  for (int q = 0; q < P; ++q) {
+    uint64_t x;
+    if (p.in_mode == 2) {
+      const uint8_t* b = reinterpret_cast<const uint8_t*>(p.in_ptr[0]) + (static_cast<size_t>(s) * P + q) * IB;
+      x = 0;
+      for (int i = 0; i < IB; ++i) x |= static_cast<uint64_t>(b[i]) << (8 * i);
+    } else if constexpr (IB == 4) {
+      x = reinterpret_cast<const uint32_t*>(p.in_ptr[q])[s];
+    } else {
+      x = reinterpret_cast<const uint8_t*>(p.in_ptr[q])[s];
+    }
+    v |= x << (8 * IB * q);
+  }
+  return static_cast<InRec>(v);
+}
+
+// The fused tick: [frozen check] [input ingestion] LOAD, then for each step
+// [SAVE (+checksum, +first-seen record/compare)] ADVANCE, [display checksum],
+// [live store], [mismatch -> freeze].
+template <class G>
+__global__ void __launch_bounds__(256) tick_kernel(const KParams p) {
+  using InRec = typename G::InRec;
+  using CS = typename G::CS;
+  constexpr int NW = G::NW;
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= p.Spad) return;
+  {
+    const int wave0 = __builtin_amdgcn_readfirstlane(s) & ~63;
+    const unsigned long long fw = p.frozen[wave0 >> 6];
+    if ((fw >> (s & 63)) & 1ull) return;  // advance_frame keeps returning Err for this session
+  }
+  if (s >= p.S) return;
+  const int Spad = p.Spad;
+  InRec* __restrict__ ring = reinterpret_cast<InRec*>(p.ring);
+  CS* __restrict__ csa = reinterpret_cast<CS*>(p.cs);
+  CS* __restrict__ fsa = reinterpret_cast<CS*>(p.fs);
+
+  // InputQueue::add_input for every handle (input_queue.rs:149-239): the
+  // delay-fill replication, then the new inputs at frame current + delay.
+  if (p.n_repl > 0) {
+    const InRec v = ring[static_cast<size_t>(p.repl_src) * Spad + s];
+    for (int r = 0; r < p.n_repl; ++r) ring[static_cast<size_t>(p.repl_dst[r]) * Spad + s] = v;
+  }
+  if (p.in_mode != 0 && p.user_slot >= 0) ring[static_cast<size_t>(p.user_slot) * Spad + s] = gather_new_input<G>(p, s);
+
+  uint32_t w[NW];
+  if (p.load_slot >= 0)
+    load_words<NW>(p.snap + static_cast<size_t>(p.load_slot) * NW * Spad, Spad, s, w);
+  else
+    load_words<NW>(p.live, Spad, s, w);
+
+  CsCtx ctx{p.seed, static_cast<uint32_t>(s), p.nonce_base};
+  int32_t mismatch = kNullFrame;
+  for (int base = 0; base < p.n_steps; base += kChunk) {
+    InRec in[kChunk];
+#pragma unroll
+    for (int k = 0; k < kChunk; ++k)
+      if (base + k < p.n_steps) in[k] = ring[static_cast<size_t>((p.f0 + base + k) & (kQueueLen - 1)) * Spad + s];
+#pragma unroll
+    for (int k = 0; k < kChunk; ++k) {
+      const int step = base + k;
+      if (step >= p.n_steps) break;
+      const int32_t f = p.f0 + step;
+      const uint32_t mode = (p.save_modes[step >> 4] >> ((step & 15) * 2)) & 3u;
+      if (mode != SAVE_NONE) {  // SaveGameState{cell, f}: checksum, cell.save
+        ctx.nonce = p.nonce_base + static_cast<uint32_t>(step);
+        const CS c = G::checksum(w, f, ctx);
+        const size_t slot = static_cast<size_t>(f % p.W);
+        store_words<NW>(p.snap + slot * NW * Spad, Spad, s, w);
+        csa[slot * Spad + s] = c;
+        if (mode == SAVE_RECORD) {
+          fsa[slot * Spad + s] = c;
+        } else if (mode == SAVE_COMPARE) {
+          if (c != fsa[slot * Spad + s]) mismatch = f;  // newest mismatching frame wins
+        }
+      }
+      G::advance(w, in[k], p.disc_mask, &p.counters[1]);  // AdvanceFrame{inputs}
+      if (step == p.periodic_step) {
+        ctx.nonce = p.nonce_base + 128u + static_cast<uint32_t>(step);
+        reinterpret_cast<CS*>(p.periodic_cs)[s] = G::checksum(w, f + 1, ctx);
+      }
+    }
+  }
+  if (p.display) {  // Game::last_checksum after the final AdvanceFrame (ex_game.rs:104-108)
+    ctx.nonce = p.nonce_base + 255u;
+    reinterpret_cast<CS*>(p.last_cs)[s] = G::checksum(w, p.f0 + p.n_steps, ctx);
+  }
+  if (p.live_out || mismatch != kNullFrame) store_words<NW>(p.live, Spad, s, w);
+  if (mismatch != kNullFrame) {
+    p.err[s] = mismatch;
+    atomicOr(&p.frozen[s >> 6], 1ull << (s & 63));
+    atomicAdd(&p.counters[0], 1u);
+  }
+}
+
+__host__ __device__ inline U128 to_u128(uint16_t c) { return U128{c, 0}; }
+__host__ __device__ inline U128 to_u128(uint64_t c) { return U128{c, 0}; }
+__host__ __device__ inline U128 to_u128(U128 c) { return c; }
+
+template <class G>
+__global__ void report_kernel(const typename G::CS* __restrict__ cs, const int32_t* __restrict__ err, int S,
+                              int32_t frame, rb_checksum_report* __restrict__ out) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= S) return;
+  const U128 c = to_u128(cs[s]);
+  rb_checksum_report r;
+  r.checksum_lo = c.lo;
+  r.checksum_hi = c.hi;
+  r.frame = frame;
+  r.mismatch_frame = err[s];
+  out[s] = r;
+}
+
+__global__ void sincos_kernel(const float* __restrict__ x, float* __restrict__ so, float* __restrict__ co, int64_t n,
+                              uint32_t* unexpected) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const SinCos r = sincosf_glibc(x[i], unexpected);
+  so[i] = r.s;
+  co[i] = r.c;
+}
+
+}  // namespace rb
+
+// ============================================================================
+// host side
+// ============================================================================
+namespace rb {
+struct GameOps {
+  virtual ~GameOps() = default;
+  int nw = 0, players = 0, input_bytes = 0, inrec_bytes = 0, cs_bytes = 0, image_bytes = 0;
+  bool display = false;
+  virtual void init_words(uint32_t* w) const = 0;
+  virtual void image(const uint32_t* w, int32_t frame, uint8_t* out) const = 0;
+  virtual U128 cs_at(const void* arr, size_t i) const = 0;
+  virtual hipError_t launch_tick(const KParams& p, int block, hipStream_t st) const = 0;
+  virtual hipError_t launch_report(const void* cs, const int32_t* err, int S, int32_t frame, void* out,
+                                   hipStream_t st) const = 0;
+};
+
+template <class G, bool kDisplay>
+struct GameOpsT final : GameOps {
+  GameOpsT() {
+    nw = G::NW;
+    players = G::kPlayers;
+    input_bytes = G::kInputBytes;
+    inrec_bytes = sizeof(typename G::InRec);
+    cs_bytes = sizeof(typename G::CS);
+    image_bytes = G::kImageBytes;
+    display = kDisplay;
+  }
+  void init_words(uint32_t* w) const override { G::init(w); }
+  void image(const uint32_t* w, int32_t frame, uint8_t* out) const override { G::image(w, frame, out); }
+  U128 cs_at(const void* arr, size_t i) const override {
+    return to_u128(reinterpret_cast<const typename G::CS*>(arr)[i]);
+  }
+  hipError_t launch_tick(const KParams& p, int block, hipStream_t st) const override {
+    const int grid = (p.Spad + block - 1) / block;
+    hipLaunchKernelGGL(tick_kernel<G>, dim3(grid), dim3(block), 0, st, p);
+    return hipGetLastError();
+  }
+  hipError_t launch_report(const void* cs, const int32_t* err, int S, int32_t frame, void* out,
+                           hipStream_t st) const override {
+    hipLaunchKernelGGL(report_kernel<G>, dim3((S + 255) / 256), dim3(256), 0, st,
+                       reinterpret_cast<const typename G::CS*>(cs), err, S, frame,
+                       reinterpret_cast<rb_checksum_report*>(out));
+    return hipGetLastError();
+  }
+};
+
+inline std::unique_ptr<GameOps> make_game(int game, int players) {
+  switch (game) {
+    case RB_GAME_EX_GAME:
+      switch (players) {
+        case 1: return std::make_unique<GameOpsT<ExGame<1>, true>>();
+        case 2: return std::make_unique<GameOpsT<ExGame<2>, true>>();
+        case 3: return std::make_unique<GameOpsT<ExGame<3>, true>>();
+        case 4: return std::make_unique<GameOpsT<ExGame<4>, true>>();
+        default: return nullptr;
+      }
+    case RB_GAME_STUB: return players == 2 ? std::make_unique<GameOpsT<StubGame, false>>() : nullptr;
+    case RB_GAME_STUB_ENUM: return players == 2 ? std::make_unique<GameOpsT<StubEnumGame, false>>() : nullptr;
+    case RB_GAME_STUB_RANDOM_CS:
+      return players == 2 ? std::make_unique<GameOpsT<StubRandomCsGame, false>>() : nullptr;
+    default: return nullptr;
+  }
+}
+
+}  // namespace rb
+
+using namespace rb;
+
+struct rb_batch {
+  rb_config cfg{};
+  std::unique_ptr<GameOps> ops;
+  std::unique_ptr<SyncTestPlan> plan;
+  int S = 0, Spad = 0, W = 0, P = 0, block = 256;
+  bool plan_only = false;
+  int device = 0;
+  hipStream_t own_stream = nullptr, stream = nullptr;
+  // device buffers
+  uint32_t* snap = nullptr;
+  uint32_t* live = nullptr;
+  void* cs = nullptr;
+  void* fs = nullptr;
+  void* ring = nullptr;
+  void* last_cs = nullptr;
+  void* periodic_cs = nullptr;
+  int32_t* err = nullptr;
+  unsigned long long* frozen = nullptr;
+  uint32_t* counters = nullptr;
+  // input staging for host pointers: [2][P][S*input_bytes]
+  uint8_t* stage_dev = nullptr;
+  uint8_t* stage_host = nullptr;
+  hipEvent_t stage_ev[2] = {nullptr, nullptr};
+  int stage_parity = 0;
+  const void* in_ptr[4] = {nullptr, nullptr, nullptr, nullptr};
+  int in_mode = 0;
+  // checked mode
+  uint32_t* pinned_counters = nullptr;
+  hipEvent_t tick_ev = nullptr;
+  bool tick_pending = false;
+  // live-state validity and bookkeeping
+  bool live_valid = true;
+  int32_t display_frame = kNullFrame;
+  uint32_t tick = 0;
+  // profiling
+  bool prof = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev;  // pool, reused after rb_profile_take
+  size_t prof_used = 0;
+  std::string last_err;
+};
+
+namespace {
+thread_local std::string g_create_err;
+
+rb_status fail(rb_batch* b, rb_status st, const std::string& msg) {
+  if (b) b->last_err = msg; else g_create_err = msg;
+  return st;
+}
+#define HIP_TRY(b, expr)                                                                          \
+  do {                                                                                            \
+    hipError_t _e = (expr);                                                                       \
+    if (_e != hipSuccess) return fail((b), RB_DEVICE_ERROR, std::string(#expr ": ") + hipGetErrorString(_e)); \
+  } while (0)
+
+rb_status destroy_device(rb_batch* b) {
+  if (b->plan_only) return RB_OK;
+  (void)hipSetDevice(b->device);
+  if (b->stream) (void)hipStreamSynchronize(b->stream);
+  void* ptrs[] = {b->snap, b->live, b->cs, b->fs, b->ring, b->last_cs, b->periodic_cs, b->err, b->frozen,
+                  b->counters, b->stage_dev};
+  for (void* q : ptrs)
+    if (q) (void)hipFree(q);
+  if (b->stage_host) (void)hipHostFree(b->stage_host);
+  if (b->pinned_counters) (void)hipHostFree(b->pinned_counters);
+  for (auto& e : b->stage_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (b->tick_ev) (void)hipEventDestroy(b->tick_ev);
+  for (auto& pr : b->prof_ev) {
+    (void)hipEventDestroy(pr.first);
+    (void)hipEventDestroy(pr.second);
+  }
+  if (b->own_stream) (void)hipStreamDestroy(b->own_stream);
+  return RB_OK;
+}
+
+rb_status launch_program(rb_batch* b, const TickProgram& tp, bool ingest, bool display, int32_t periodic_step) {
+  KParams p{};
+  p.snap = b->snap;
+  p.live = b->live;
+  p.cs = b->cs;
+  p.fs = b->fs;
+  p.ring = b->ring;
+  p.last_cs = b->last_cs;
+  p.periodic_cs = b->periodic_cs;
+  p.err = b->err;
+  p.frozen = b->frozen;
+  p.counters = b->counters;
+  p.S = b->S;
+  p.Spad = b->Spad;
+  p.W = b->W;
+  if (ingest) {
+    p.in_mode = b->in_mode;
+    for (int i = 0; i < 4; ++i) p.in_ptr[i] = b->in_ptr[i];
+    p.user_slot = tp.user_slot;
+    p.n_repl = static_cast<int32_t>(tp.repl_dst.size());
+    if (p.n_repl > kMaxRepl) return fail(b, RB_INVALID_REQUEST, "input delay above 8 is not supported by the device batch");
+    for (int i = 0; i < p.n_repl; ++i) p.repl_dst[i] = tp.repl_dst[i];
+    p.repl_src = tp.repl_src;
+  } else {
+    p.in_mode = 0;
+    p.user_slot = -1;
+  }
+  p.load_slot = tp.load ? tp.load_frame % b->W : -1;
+  p.f0 = tp.f0;
+  p.n_steps = tp.n_steps;
+  for (int k = 0; k < tp.n_steps; ++k) p.save_modes[k >> 4] |= static_cast<uint32_t>(tp.save_mode[k] & 3u) << ((k & 15) * 2);
+  p.live_out = tp.live_out ? 1 : 0;
+  p.periodic_step = periodic_step;
+  p.display = display ? 1 : 0;
+  p.disc_mask = 0;
+  p.seed = b->cfg.seed;
+  p.nonce_base = (b->tick & 0xffffffu) << 8;
+  if (b->prof) {
+    if (b->prof_used == b->prof_ev.size()) {
+      hipEvent_t e0 = nullptr, e1 = nullptr;
+      HIP_TRY(b, hipEventCreate(&e0));
+      HIP_TRY(b, hipEventCreate(&e1));
+      b->prof_ev.push_back({e0, e1});
+    }
+    HIP_TRY(b, hipEventRecord(b->prof_ev[b->prof_used].first, b->stream));
+  }
+  HIP_TRY(b, b->ops->launch_tick(p, b->block, b->stream));
+  if (b->prof) {
+    HIP_TRY(b, hipEventRecord(b->prof_ev[b->prof_used].second, b->stream));
+    b->prof_used += 1;
+  }
+  return RB_OK;
+}
+
+rb_status read_words_slot(rb_batch* b, const uint32_t* dev_base, std::vector<uint32_t>& host) {
+  host.resize(static_cast<size_t>(b->ops->nw) * b->Spad);
+  HIP_TRY(b, hipMemcpyAsync(host.data(), dev_base, host.size() * 4, hipMemcpyDeviceToHost, b->stream));
+  HIP_TRY(b, hipStreamSynchronize(b->stream));
+  return RB_OK;
+}
+
+void words_of(const rb_batch* b, const std::vector<uint32_t>& planes, int s, uint32_t* w) {
+  for (int k = 0; k < b->ops->nw; ++k) w[k] = planes[word_index(b->ops->nw, b->Spad, s, k)];
+}
+
+}  // namespace
+
+extern "C" {
+
+void rb_config_init(rb_config* c) {
+  std::memset(c, 0, sizeof(*c));
+  c->abi_version = RB_ABI_VERSION;
+  c->game = RB_GAME_EX_GAME;
+  c->num_sessions = 1;
+  c->num_players = 2;     // builder.rs:13
+  c->max_prediction = 8;  // builder.rs:20
+  c->check_distance = 2;  // builder.rs:21
+  c->input_delay = 0;     // builder.rs:16
+  c->device = 0;
+  c->flags = RB_FLAG_CHECKED;
+}
+
+const char* rb_last_error(const rb_batch* b) { return b ? b->last_err.c_str() : g_create_err.c_str(); }
+
+rb_status rb_synctest_create(const rb_config* cfg, rb_batch** out) {
+  *out = nullptr;
+  if (!cfg || cfg->abi_version != RB_ABI_VERSION) return fail(nullptr, RB_INVALID_REQUEST, "rb_config.abi_version mismatch");
+  // builder.rs:136-145
+  if (cfg->max_prediction <= 0)
+    return fail(nullptr, RB_INVALID_REQUEST, "Currently, only prediction windows above 0 are supported");
+  if (cfg->check_distance < 0 || cfg->input_delay < 0 || cfg->num_players <= 0 || cfg->num_sessions <= 0)
+    return fail(nullptr, RB_INVALID_REQUEST, "negative or zero size in rb_config");
+  // builder.rs:342-347
+  if (cfg->check_distance >= cfg->max_prediction) return fail(nullptr, RB_INVALID_REQUEST, "Check distance too big.");
+  if (cfg->max_prediction > kMaxSteps)
+    return fail(nullptr, RB_INVALID_REQUEST, "max_prediction above 64 is not supported by the device batch");
+  if (cfg->input_delay > kQueueLen - cfg->max_prediction - 2)
+    return fail(nullptr, RB_INVALID_REQUEST, "input delay does not fit the 128-entry input queue");
+  auto ops = make_game(cfg->game, cfg->num_players);
+  if (!ops) return fail(nullptr, RB_INVALID_REQUEST, "unsupported game / num_players combination");
+
+  auto b = std::make_unique<rb_batch>();
+  b->cfg = *cfg;
+  b->ops = std::move(ops);
+  b->plan = std::make_unique<SyncTestPlan>(cfg->num_players, cfg->max_prediction, cfg->check_distance, cfg->input_delay);
+  b->S = cfg->num_sessions;
+  b->Spad = (cfg->num_sessions + 63) / 64 * 64;
+  b->W = cfg->max_prediction;
+  b->P = cfg->num_players;
+  b->block = cfg->block_size ? static_cast<int>(cfg->block_size) : 256;
+  if (b->block % 64 != 0 || b->block > 256) return fail(nullptr, RB_INVALID_REQUEST, "block_size must be 64, 128, 192 or 256");
+  b->plan_only = cfg->device < 0;
+  b->device = cfg->device;
+  if (b->plan_only) {
+    *out = b.release();
+    return RB_OK;
+  }
+  rb_batch* bp = b.get();
+  auto hip_fail = [&](hipError_t e, const char* what) {
+    g_create_err = std::string(what) + ": " + hipGetErrorString(e);
+    destroy_device(bp);
+    return RB_DEVICE_ERROR;
+  };
+#define HIP_CREATE(expr)                          \
+  do {                                            \
+    hipError_t _e = (expr);                       \
+    if (_e != hipSuccess) return hip_fail(_e, #expr); \
+  } while (0)
+  HIP_CREATE(hipSetDevice(b->device));
+  HIP_CREATE(hipStreamCreateWithFlags(&b->own_stream, hipStreamNonBlocking));
+  b->stream = b->own_stream;
+  const size_t Sp = b->Spad, NW = b->ops->nw, W = b->W;
+  HIP_CREATE(hipMalloc(&b->snap, W * NW * Sp * 4));
+  HIP_CREATE(hipMalloc(&b->live, NW * Sp * 4));
+  HIP_CREATE(hipMalloc(&b->cs, W * Sp * b->ops->cs_bytes));
+  HIP_CREATE(hipMalloc(&b->fs, W * Sp * b->ops->cs_bytes));
+  HIP_CREATE(hipMalloc(&b->ring, kQueueLen * Sp * b->ops->inrec_bytes));
+  HIP_CREATE(hipMalloc(&b->last_cs, Sp * b->ops->cs_bytes));
+  HIP_CREATE(hipMalloc(&b->periodic_cs, Sp * b->ops->cs_bytes));
+  HIP_CREATE(hipMalloc(&b->err, Sp * 4));
+  HIP_CREATE(hipMalloc(&b->frozen, Sp / 64 * 8));
+  HIP_CREATE(hipMalloc(&b->counters, 16));
+  const size_t stage = 2ull * b->P * Sp * b->ops->input_bytes;
+  HIP_CREATE(hipMalloc(&b->stage_dev, stage));
+  HIP_CREATE(hipHostMalloc(&b->stage_host, stage));
+  HIP_CREATE(hipHostMalloc(&b->pinned_counters, 16));
+  HIP_CREATE(hipEventCreateWithFlags(&b->stage_ev[0], hipEventDisableTiming));
+  HIP_CREATE(hipEventCreateWithFlags(&b->stage_ev[1], hipEventDisableTiming));
+  HIP_CREATE(hipEventCreateWithFlags(&b->tick_ev, hipEventDisableTiming));
+  HIP_CREATE(hipMemsetAsync(b->snap, 0, W * NW * Sp * 4, b->stream));
+  HIP_CREATE(hipMemsetAsync(b->cs, 0, W * Sp * b->ops->cs_bytes, b->stream));
+  HIP_CREATE(hipMemsetAsync(b->fs, 0, W * Sp * b->ops->cs_bytes, b->stream));
+  HIP_CREATE(hipMemsetAsync(b->ring, 0, kQueueLen * Sp * b->ops->inrec_bytes, b->stream));  // blank inputs
+  HIP_CREATE(hipMemsetAsync(b->last_cs, 0, Sp * b->ops->cs_bytes, b->stream));
+  HIP_CREATE(hipMemsetAsync(b->periodic_cs, 0, Sp * b->ops->cs_bytes, b->stream));
+  HIP_CREATE(hipMemsetAsync(b->err, 0xff, Sp * 4, b->stream));  // NULL_FRAME
+  HIP_CREATE(hipMemsetAsync(b->frozen, 0, Sp / 64 * 8, b->stream));
+  HIP_CREATE(hipMemsetAsync(b->counters, 0, 16, b->stream));
+  // State::new for every session (ex_game.rs:234-257), host-evaluated once.
+  std::vector<uint32_t> w0(NW), planes(NW * Sp);
+  b->ops->init_words(w0.data());
+  for (size_t s = 0; s < Sp; ++s)
+    for (size_t k = 0; k < NW; ++k) planes[word_index(static_cast<int>(NW), b->Spad, static_cast<int>(s), static_cast<int>(k))] = w0[k];
+  HIP_CREATE(hipMemcpyAsync(b->live, planes.data(), planes.size() * 4, hipMemcpyHostToDevice, b->stream));
+  HIP_CREATE(hipStreamSynchronize(b->stream));
+#undef HIP_CREATE
+  *out = b.release();
+  return RB_OK;
+}
+
+void rb_destroy(rb_batch* b) {
+  if (!b) return;
+  destroy_device(b);
+  delete b;
+}
+
+rb_status rb_set_stream(rb_batch* b, void* s) {
+  if (b->plan_only) return RB_OK;
+  HIP_TRY(b, hipStreamSynchronize(b->stream));
+  b->stream = s ? static_cast<hipStream_t>(s) : b->own_stream;
+  return RB_OK;
+}
+
+int32_t rb_current_frame(const rb_batch* b) { return b->plan->current; }
+int32_t rb_num_sessions(const rb_batch* b) { return b->S; }
+int32_t rb_state_bytes(const rb_batch* b) { return b->ops->image_bytes; }
+int32_t rb_input_bytes(const rb_batch* b) { return b->ops->input_bytes; }
+
+rb_status rb_add_local_input(rb_batch* b, int32_t handle, const void* inputs, int32_t on_device) {
+  // sync_test_session.rs:66-70
+  if (!b->plan->add_local_input(handle))
+    return fail(b, RB_INVALID_REQUEST, "The player handle you provided is not valid.");
+  if (b->plan_only) return RB_OK;
+  if (handle >= 4) return fail(b, RB_INVALID_REQUEST, "at most 4 players per session");
+  if (b->in_mode == 2) {  // switching from packed: every handle must be given again
+    for (auto& q : b->in_ptr) q = nullptr;
+  }
+  b->in_mode = 1;
+  if (on_device) {
+    b->in_ptr[handle] = inputs;
+    return RB_OK;
+  }
+  const size_t bytes = static_cast<size_t>(b->S) * b->ops->input_bytes;
+  const size_t off = (static_cast<size_t>(b->stage_parity) * b->P + handle) * b->Spad * b->ops->input_bytes;
+  HIP_TRY(b, hipEventSynchronize(b->stage_ev[b->stage_parity]));  // previous copy out of this slot is done
+  std::memcpy(b->stage_host + off, inputs, bytes);
+  HIP_TRY(b, hipMemcpyAsync(b->stage_dev + off, b->stage_host + off, bytes, hipMemcpyHostToDevice, b->stream));
+  b->in_ptr[handle] = b->stage_dev + off;
+  return RB_OK;
+}
+
+rb_status rb_add_local_inputs_packed(rb_batch* b, const void* inputs, int32_t on_device) {
+  for (int h = 0; h < b->P; ++h) b->plan->add_local_input(h);
+  if (b->plan_only) return RB_OK;
+  b->in_mode = 2;
+  if (on_device) {
+    b->in_ptr[0] = inputs;
+    return RB_OK;
+  }
+  const size_t bytes = static_cast<size_t>(b->S) * b->P * b->ops->input_bytes;
+  const size_t off = static_cast<size_t>(b->stage_parity) * b->P * b->Spad * b->ops->input_bytes;
+  HIP_TRY(b, hipEventSynchronize(b->stage_ev[b->stage_parity]));
+  std::memcpy(b->stage_host + off, inputs, bytes);
+  HIP_TRY(b, hipMemcpyAsync(b->stage_dev + off, b->stage_host + off, bytes, hipMemcpyHostToDevice, b->stream));
+  b->in_ptr[0] = b->stage_dev + off;
+  return RB_OK;
+}
+
+rb_status rb_advance_frame(rb_batch* b) {
+  rb_status result = RB_OK;
+  // Checked mode: sessions frozen by the previous tick fail this call
+  // (sync_test_session.rs:91-98 returns MismatchedChecksum before any work).
+  if (!b->plan_only && (b->cfg.flags & RB_FLAG_CHECKED) && b->tick_pending) {
+    HIP_TRY(b, hipEventSynchronize(b->tick_ev));
+    b->tick_pending = false;
+    if (b->pinned_counters[0] > 0) result = RB_MISMATCHED_CHECKSUM;
+  }
+  TickProgram tp;
+  std::string info;
+  int rc;
+  try {
+    rc = b->plan->advance(tp, info);
+  } catch (const Panic& e) {
+    return fail(b, RB_PANIC, e.what());
+  }
+  if (rc == 2) return fail(b, RB_INVALID_REQUEST, info);
+  if (rc == 1) return fail(b, RB_PREDICTION_THRESHOLD, "Prediction threshold is reached, cannot proceed without catching up.");
+  if (b->plan_only) return result;
+  if (b->in_mode == 1)
+    for (int h = 0; h < b->P; ++h)
+      if (!b->in_ptr[h]) return fail(b, RB_PANIC, "input pointer missing for a handle");
+  // ex_game's periodic checksum: frame % CHECKSUM_PERIOD == 0 after an advance (ex_game.rs:109-111)
+  int32_t periodic_step = -1;
+  if (b->ops->display)
+    for (int k = 0; k < tp.n_steps; ++k)
+      if ((tp.f0 + k + 1) % 100 == 0) periodic_step = k;
+  rb_status st = launch_program(b, tp, true, b->ops->display, periodic_step);
+  if (st != RB_OK) return st;
+  // the staging slot used by this tick may be refilled once this point passes
+  HIP_TRY(b, hipEventRecord(b->stage_ev[b->stage_parity], b->stream));
+  b->stage_parity ^= 1;
+  b->in_mode = 0;
+  for (auto& q : b->in_ptr) q = nullptr;
+  b->live_valid = tp.live_out;
+  b->display_frame = tp.f0 + tp.n_steps;
+  b->tick += 1;
+  if (b->cfg.flags & RB_FLAG_CHECKED) {
+    HIP_TRY(b, hipMemcpyAsync(b->pinned_counters, b->counters, 8, hipMemcpyDeviceToHost, b->stream));
+    HIP_TRY(b, hipEventRecord(b->tick_ev, b->stream));
+    b->tick_pending = true;
+  }
+  if (result != RB_OK) b->last_err = "Detected checksum mismatch during rollback (see rb_mismatches).";
+  return result;
+}
+
+rb_status rb_synchronize(rb_batch* b) {
+  if (b->plan_only) return RB_OK;
+  HIP_TRY(b, hipStreamSynchronize(b->stream));
+  return RB_OK;
+}
+
+rb_status rb_mismatches(rb_batch* b, int32_t* frames_out, int32_t* count_out) {
+  if (b->plan_only) {
+    if (count_out) *count_out = 0;
+    return RB_OK;
+  }
+  std::vector<int32_t> e(b->Spad);
+  HIP_TRY(b, hipMemcpyAsync(e.data(), b->err, b->Spad * 4, hipMemcpyDeviceToHost, b->stream));
+  HIP_TRY(b, hipStreamSynchronize(b->stream));
+  int32_t n = 0;
+  for (int s = 0; s < b->S; ++s) {
+    if (e[s] != kNullFrame) ++n;
+    if (frames_out) frames_out[s] = e[s];
+  }
+  if (count_out) *count_out = n;
+  return RB_OK;
+}
+
+int32_t rb_last_requests(const rb_batch* b, int32_t* kinds, int32_t* frames, int32_t cap) {
+  const auto& t = b->plan->trace;
+  const int32_t n = static_cast<int32_t>(t.size());
+  for (int32_t i = 0; i < n && i < cap; ++i) {
+    if (kinds) kinds[i] = t[i].kind;
+    if (frames) frames[i] = t[i].frame;
+  }
+  return n;
+}
+
+rb_status rb_read_cell(rb_batch* b, int32_t frame, void* images, uint64_t* checksums) {
+  if (b->plan_only) return fail(b, RB_INVALID_REQUEST, "plan-only batch holds no states");
+  if (frame < 0 || b->plan->cell_frame[frame % b->W] != frame)
+    return fail(b, RB_INVALID_REQUEST, "no cell holds frame " + std::to_string(frame));
+  const size_t slot = static_cast<size_t>(frame % b->W);
+  std::vector<uint32_t> planes;
+  rb_status st = read_words_slot(b, b->snap + slot * b->ops->nw * b->Spad, planes);
+  if (st != RB_OK) return st;
+  std::vector<uint8_t> csh(static_cast<size_t>(b->Spad) * b->ops->cs_bytes);
+  HIP_TRY(b, hipMemcpy(csh.data(), static_cast<uint8_t*>(b->cs) + slot * b->Spad * b->ops->cs_bytes, csh.size(),
+                       hipMemcpyDeviceToHost));
+  std::vector<uint32_t> w(b->ops->nw);
+  for (int s = 0; s < b->S; ++s) {
+    words_of(b, planes, s, w.data());
+    if (images) b->ops->image(w.data(), frame, static_cast<uint8_t*>(images) + static_cast<size_t>(s) * b->ops->image_bytes);
+    if (checksums) {
+      U128 c = b->ops->cs_at(csh.data(), s);
+      checksums[2 * s] = c.lo;
+      checksums[2 * s + 1] = c.hi;
+    }
+  }
+  return RB_OK;
+}
+
+rb_status rb_read_live(rb_batch* b, void* images, uint64_t* display_checksums, int32_t* display_frame) {
+  if (b->plan_only) return fail(b, RB_INVALID_REQUEST, "plan-only batch holds no states");
+  const int32_t cur = b->plan->current;
+  if (!b->live_valid) {
+    // The last tick ended right before a LoadGameState, so its final state
+    // was not stored: replay it from the cell it saved (frame cur-1) and the
+    // confirmed input of that frame.  Deterministic, touches nothing else.
+    TickProgram tp;
+    tp.load = true;
+    tp.load_frame = cur - 1;
+    tp.f0 = cur - 1;
+    tp.n_steps = 1;
+    tp.live_out = true;
+    if (b->plan->cell_frame[(cur - 1) % b->W] != cur - 1)
+      return fail(b, RB_PANIC, "live-state replay: cell for the last frame is missing");
+    rb_status st = launch_program(b, tp, false, false, -1);
+    if (st != RB_OK) return st;
+    b->live_valid = true;
+  }
+  std::vector<uint32_t> planes;
+  rb_status st = read_words_slot(b, b->live, planes);
+  if (st != RB_OK) return st;
+  std::vector<uint8_t> dcs(static_cast<size_t>(b->Spad) * b->ops->cs_bytes);
+  HIP_TRY(b, hipMemcpy(dcs.data(), b->last_cs, dcs.size(), hipMemcpyDeviceToHost));
+  std::vector<int32_t> e(b->Spad);
+  HIP_TRY(b, hipMemcpy(e.data(), b->err, b->Spad * 4, hipMemcpyDeviceToHost));
+  std::vector<uint32_t> w(b->ops->nw);
+  for (int s = 0; s < b->S; ++s) {
+    words_of(b, planes, s, w.data());
+    // a failed session stopped advancing at the end of the tick that detected it
+    if (images) b->ops->image(w.data(), cur, static_cast<uint8_t*>(images) + static_cast<size_t>(s) * b->ops->image_bytes);
+    if (display_checksums) display_checksums[s] = b->ops->display ? b->ops->cs_at(dcs.data(), s).lo : 0;
+  }
+  if (display_frame) *display_frame = b->ops->display ? b->display_frame : kNullFrame;
+  return RB_OK;
+}
+
+rb_status rb_export_checksum_report(rb_batch* b, int32_t frame, void* dev_out) {
+  if (b->plan_only) return fail(b, RB_INVALID_REQUEST, "plan-only batch holds no states");
+  if (frame < 0 || b->plan->cell_frame[frame % b->W] != frame)
+    return fail(b, RB_INVALID_REQUEST, "no cell holds frame " + std::to_string(frame));
+  const size_t slot = static_cast<size_t>(frame % b->W);
+  HIP_TRY(b, b->ops->launch_report(static_cast<uint8_t*>(b->cs) + slot * b->Spad * b->ops->cs_bytes, b->err, b->S,
+                                   frame, dev_out, b->stream));
+  return RB_OK;
+}
+
+rb_status rb_debug_corrupt_cell(rb_batch* b, int32_t session, int32_t frame, int32_t word, uint32_t xor_mask) {
+  if (b->plan_only) return fail(b, RB_INVALID_REQUEST, "plan-only batch holds no states");
+  if (session < 0 || session >= b->S || word < 0 || word >= b->ops->nw)
+    return fail(b, RB_INVALID_REQUEST, "session/word out of range");
+  if (frame < 0 || b->plan->cell_frame[frame % b->W] != frame)
+    return fail(b, RB_INVALID_REQUEST, "no cell holds frame " + std::to_string(frame));
+  uint32_t* p = b->snap + static_cast<size_t>(frame % b->W) * b->ops->nw * b->Spad +
+                word_index(b->ops->nw, b->Spad, session, word);
+  uint32_t v;
+  HIP_TRY(b, hipStreamSynchronize(b->stream));
+  HIP_TRY(b, hipMemcpy(&v, p, 4, hipMemcpyDeviceToHost));
+  v ^= xor_mask;
+  HIP_TRY(b, hipMemcpy(p, &v, 4, hipMemcpyHostToDevice));
+  return RB_OK;
+}
+
+rb_status rb_debug_sincosf(int32_t device, const float* x, float* so, float* co, int64_t n) {
+  rb_batch* b = nullptr;
+  if (n <= 0) return RB_OK;
+  HIP_TRY(b, hipSetDevice(device));
+  float *dx = nullptr, *ds = nullptr, *dc = nullptr;
+  uint32_t* du = nullptr;
+  const size_t bytes = static_cast<size_t>(n) * 4;
+  hipError_t e = hipMalloc(&dx, bytes);
+  if (e == hipSuccess) e = hipMalloc(&ds, bytes);
+  if (e == hipSuccess) e = hipMalloc(&dc, bytes);
+  if (e == hipSuccess) e = hipMalloc(&du, 4);
+  if (e == hipSuccess) e = hipMemset(du, 0, 4);
+  if (e == hipSuccess) e = hipMemcpy(dx, x, bytes, hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(sincos_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, nullptr, dx, ds, dc, n, du);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpy(so, ds, bytes, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(co, dc, bytes, hipMemcpyDeviceToHost);
+  (void)hipFree(dx);
+  (void)hipFree(ds);
+  (void)hipFree(dc);
+  (void)hipFree(du);
+  if (e != hipSuccess) return fail(nullptr, RB_DEVICE_ERROR, std::string("rb_debug_sincosf: ") + hipGetErrorString(e));
+  return RB_OK;
+}
+
+rb_status rb_profile_enable(rb_batch* b, int32_t on) {
+  b->prof = on != 0;
+  return RB_OK;
+}
+
+rb_status rb_profile_take(rb_batch* b, double* total_ms, int32_t* launches) {
+  double t = 0;
+  if (!b->plan_only && b->prof_used > 0) {
+    HIP_TRY(b, hipEventSynchronize(b->prof_ev[b->prof_used - 1].second));
+    for (size_t i = 0; i < b->prof_used; ++i) {
+      float ms = 0;
+      HIP_TRY(b, hipEventElapsedTime(&ms, b->prof_ev[i].first, b->prof_ev[i].second));
+      t += ms;
+    }
+  }
+  if (total_ms) *total_ms = t;
+  if (launches) *launches = static_cast<int32_t>(b->prof_used);
+  b->prof_used = 0;
+  return RB_OK;
+}
+
+}  // extern "C"

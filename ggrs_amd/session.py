@@ -1,0 +1,335 @@
+"""Host-side mirror of the GGRS session API over the C ABI.
+
+Same names, argument meaning and error behaviour as the reference
+(``SessionBuilder`` builder.rs:32-377, ``SyncTestSession``
+sync_test_session.rs:11-204, ``GGRSError`` error.rs:11-36,
+``GGRSRequest`` lib.rs:170-194), batched: one object drives ``num_sessions``
+independent sessions in lock-step on one GPU, and ``advance_frame`` executes
+the request stream it returns on the device (the game handler is compiled in,
+selected by ``Game``).
+"""
+from __future__ import annotations
+
+import ctypes
+import enum
+from collections import namedtuple
+from typing import List, Optional
+
+import numpy as np
+
+from . import _lib as L
+
+
+# --------------------------------------------------------------------------- errors (error.rs)
+class GGRSError(Exception):
+    """Base of the reference's GGRSError variants."""
+
+
+class PredictionThreshold(GGRSError):
+    """error.rs:13"""
+
+
+class InvalidRequest(GGRSError):
+    """error.rs:15-18; ``info`` carries the reference's message."""
+
+    def __init__(self, info: str):
+        super().__init__(f"Invalid Request: {info}")
+        self.info = info
+
+
+class MismatchedChecksum(GGRSError):
+    """error.rs:22-25.  Batched: ``frames[s]`` is the frame reported by session s
+    (``NULL_FRAME`` for sessions that advanced), ``frame`` the first failing one."""
+
+    def __init__(self, frames: np.ndarray):
+        failed = np.nonzero(frames != NULL_FRAME)[0]
+        self.frames = frames
+        self.sessions = failed
+        self.frame = int(frames[failed[0]]) if failed.size else NULL_FRAME
+        super().__init__(f"Detected checksum mismatch during rollback on frame {self.frame} "
+                         f"({failed.size} session(s)).")
+
+
+class NotSynchronized(GGRSError):
+    """error.rs:27"""
+
+
+class SpectatorTooFarBehind(GGRSError):
+    """error.rs:29"""
+
+
+class DeviceError(GGRSError):
+    """HIP runtime failure (no reference analogue)."""
+
+
+class Panic(GGRSError):
+    """A condition the reference enforces with assert!/panic!."""
+
+
+NULL_FRAME = L.RB_NULL_FRAME
+
+
+class InputStatus(enum.IntEnum):  # lib.rs:104-112
+    Confirmed = 0
+    Predicted = 1
+    Disconnected = 2
+
+
+class RequestKind(enum.IntEnum):  # lib.rs:170-194
+    SaveGameState = 0
+    LoadGameState = 1
+    AdvanceFrame = 2
+
+
+# (kind, frame): Save/Load carry the cell's frame; AdvanceFrame carries the
+# frame it advances from (the reference's AdvanceFrame carries the inputs).
+GGRSRequest = namedtuple("GGRSRequest", ["kind", "frame"])
+
+
+class Game(enum.IntEnum):
+    EX_GAME = L.RB_GAME_EX_GAME
+    STUB = L.RB_GAME_STUB
+    STUB_ENUM = L.RB_GAME_STUB_ENUM
+    STUB_RANDOM_CS = L.RB_GAME_STUB_RANDOM_CS
+
+
+INPUT_DTYPE = {Game.EX_GAME: np.uint8, Game.STUB: np.uint32, Game.STUB_ENUM: np.uint8,
+               Game.STUB_RANDOM_CS: np.uint32}
+
+
+def _raise(lib, handle, status: int):
+    if status == L.RB_OK:
+        return
+    msg = (lib.rb_last_error(handle) or b"").decode()
+    if status == L.RB_INVALID_REQUEST:
+        raise InvalidRequest(msg)
+    if status == L.RB_PREDICTION_THRESHOLD:
+        raise PredictionThreshold(msg)
+    if status == L.RB_NOT_SYNCHRONIZED:
+        raise NotSynchronized(msg)
+    if status == L.RB_SPECTATOR_TOO_FAR_BEHIND:
+        raise SpectatorTooFarBehind(msg)
+    if status == L.RB_DEVICE_ERROR:
+        raise DeviceError(msg)
+    raise Panic(msg or f"rb_status {status}")
+
+
+# --------------------------------------------------------------------------- builder (builder.rs)
+class SessionBuilder:
+    """builder.rs:32-377, SyncTest subset, plus the batch size and device."""
+
+    def __init__(self, game: Game = Game.EX_GAME, num_sessions: int = 1, device: int = 0):
+        self._cfg = L.RbConfig()
+        L.load().rb_config_init(ctypes.byref(self._cfg))
+        self._cfg.game = int(game)
+        self._cfg.num_sessions = int(num_sessions)
+        self._cfg.device = int(device)
+
+    def with_num_players(self, num_players: int) -> "SessionBuilder":  # :154-157
+        self._cfg.num_players = int(num_players)
+        return self
+
+    def with_max_prediction_window(self, window: int) -> "SessionBuilder":  # :136-145
+        if window == 0:
+            raise InvalidRequest("Currently, only prediction windows above 0 are supported")
+        self._cfg.max_prediction = int(window)
+        return self
+
+    def with_input_delay(self, delay: int) -> "SessionBuilder":  # :148-151
+        self._cfg.input_delay = int(delay)
+        return self
+
+    def with_check_distance(self, check_distance: int) -> "SessionBuilder":  # :202-205
+        self._cfg.check_distance = int(check_distance)
+        return self
+
+    def with_num_sessions(self, num_sessions: int) -> "SessionBuilder":
+        self._cfg.num_sessions = int(num_sessions)
+        return self
+
+    def with_device(self, device: int) -> "SessionBuilder":
+        """HIP device ordinal; -1 builds a plan-only batch (host bookkeeping only)."""
+        self._cfg.device = int(device)
+        return self
+
+    def with_checked_mismatches(self, checked: bool) -> "SessionBuilder":
+        """True (default): advance_frame raises MismatchedChecksum in the call
+        the reference would (one host/device sync per call).  False: fully
+        asynchronous ticks; read failures with ``mismatches()``."""
+        if checked:
+            self._cfg.flags |= L.RB_FLAG_CHECKED
+        else:
+            self._cfg.flags &= ~L.RB_FLAG_CHECKED
+        return self
+
+    def with_seed(self, seed: int) -> "SessionBuilder":
+        self._cfg.seed = int(seed) & (2**64 - 1)
+        return self
+
+    def with_block_size(self, block: int) -> "SessionBuilder":
+        self._cfg.block_size = int(block)
+        return self
+
+    def start_synctest_session(self) -> "SyncTestSession":  # :342-354
+        lib = L.load()
+        h = ctypes.c_void_p()
+        st = lib.rb_synctest_create(ctypes.byref(self._cfg), ctypes.byref(h))
+        _raise(lib, None, st)
+        return SyncTestSession(lib, h, Game(self._cfg.game), self._cfg)
+
+
+# --------------------------------------------------------------------------- session
+class SyncTestSession:
+    """sync_test_session.rs:11-204 for ``num_sessions`` sessions at once."""
+
+    def __init__(self, lib, handle, game: Game, cfg):
+        self._lib = lib
+        self._h = handle
+        self.game = game
+        self.num_sessions = int(cfg.num_sessions)
+        self._num_players = int(cfg.num_players)
+        self._max_prediction = int(cfg.max_prediction)
+        self.check_distance = int(cfg.check_distance)
+        self.input_delay = int(cfg.input_delay)
+        self.checked = bool(cfg.flags & L.RB_FLAG_CHECKED)
+        self.state_bytes = lib.rb_state_bytes(handle)
+        self.input_dtype = INPUT_DTYPE[game]
+        self._keep = []  # host arrays referenced by queued copies
+
+    # -- lifetime
+    def close(self):
+        if self._h:
+            self._lib.rb_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # -- reference API
+    def num_players(self) -> int:  # :149-151
+        return self._num_players
+
+    def max_prediction(self) -> int:  # :154-156
+        return self._max_prediction
+
+    def current_frame(self) -> int:
+        return self._lib.rb_current_frame(self._h)
+
+    def _as_input(self, inputs, count):
+        """numpy/int -> (pointer, on_device, keepalive); torch CUDA tensors pass through."""
+        if hasattr(inputs, "data_ptr") and getattr(inputs, "is_cuda", False):
+            if inputs.numel() != count or not inputs.is_contiguous():
+                raise InvalidRequest("device inputs must be a contiguous tensor of num_sessions values")
+            if inputs.element_size() != np.dtype(self.input_dtype).itemsize:
+                raise InvalidRequest("device inputs have the wrong element size for this game's Input")
+            return ctypes.c_void_p(inputs.data_ptr()), 1, inputs
+        arr = np.ascontiguousarray(np.broadcast_to(np.asarray(inputs), (count,)), dtype=self.input_dtype)
+        return arr.ctypes.data_as(ctypes.c_void_p), 0, arr
+
+    def add_local_input(self, player_handle: int, inputs) -> None:  # :61-74
+        """Input of ``player_handle`` for the current frame in every session:
+        an array of num_sessions values, a scalar (same input everywhere) or a
+        CUDA tensor (stays on the device)."""
+        ptr, dev, keep = self._as_input(inputs, self.num_sessions)
+        self._keep.append(keep)
+        _raise(self._lib, self._h, self._lib.rb_add_local_input(self._h, int(player_handle), ptr, dev))
+
+    def add_local_inputs(self, inputs) -> None:
+        """All handles at once: [num_sessions, num_players] values."""
+        ptr, dev, keep = self._as_input(inputs, self.num_sessions * self._num_players)
+        self._keep.append(keep)
+        _raise(self._lib, self._h, self._lib.rb_add_local_inputs_packed(self._h, ptr, dev))
+
+    def advance_frame(self) -> List[GGRSRequest]:  # :85-146
+        """Runs SyncTestSession::advance_frame and the game's handle_requests
+        for every session; returns the request stream that was executed."""
+        st = self._lib.rb_advance_frame(self._h)
+        self._keep.clear()
+        if st == L.RB_MISMATCHED_CHECKSUM:
+            raise MismatchedChecksum(self.mismatches())
+        _raise(self._lib, self._h, st)
+        return self.last_requests()
+
+    # -- batch extras
+    def last_requests(self) -> List[GGRSRequest]:
+        cap = 4 * self._max_prediction + 8
+        k = (ctypes.c_int32 * cap)()
+        f = (ctypes.c_int32 * cap)()
+        n = self._lib.rb_last_requests(self._h, k, f, cap)
+        return [GGRSRequest(RequestKind(k[i]), f[i]) for i in range(n)]
+
+    def mismatches(self) -> np.ndarray:
+        out = np.empty(self.num_sessions, dtype=np.int32)
+        cnt = ctypes.c_int32()
+        _raise(self._lib, self._h, self._lib.rb_mismatches(
+            self._h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), ctypes.byref(cnt)))
+        return out
+
+    def synchronize(self) -> None:
+        _raise(self._lib, self._h, self._lib.rb_synchronize(self._h))
+
+    def set_stream(self, stream) -> None:
+        """Run on a caller stream (int handle or torch.cuda.Stream)."""
+        ptr = getattr(stream, "cuda_stream", stream)
+        _raise(self._lib, self._h, self._lib.rb_set_stream(self._h, ctypes.c_void_p(ptr)))
+
+    def read_cell(self, frame: int):
+        """(images [S, state_bytes] u8, checksums [S, 2] u64 lo/hi) of the cell holding ``frame``."""
+        img = np.empty((self.num_sessions, self.state_bytes), dtype=np.uint8)
+        cs = np.empty((self.num_sessions, 2), dtype=np.uint64)
+        _raise(self._lib, self._h, self._lib.rb_read_cell(
+            self._h, int(frame), img.ctypes.data_as(ctypes.c_void_p),
+            cs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))))
+        return img, cs
+
+    def read_live(self):
+        """(images [S, state_bytes], display checksums [S] u64, display frame)."""
+        img = np.empty((self.num_sessions, self.state_bytes), dtype=np.uint8)
+        dcs = np.empty(self.num_sessions, dtype=np.uint64)
+        fr = ctypes.c_int32()
+        _raise(self._lib, self._h, self._lib.rb_read_live(
+            self._h, img.ctypes.data_as(ctypes.c_void_p),
+            dcs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), ctypes.byref(fr)))
+        return img, dcs, fr.value
+
+    def export_checksum_report(self, frame: int, dev_ptr: int) -> None:
+        """Write [S] rb_checksum_report (32 B each) for ``frame`` to device memory."""
+        _raise(self._lib, self._h, self._lib.rb_export_checksum_report(self._h, int(frame), ctypes.c_void_p(dev_ptr)))
+
+    def debug_corrupt_cell(self, session: int, frame: int, word: int, xor_mask: int) -> None:
+        _raise(self._lib, self._h, self._lib.rb_debug_corrupt_cell(
+            self._h, int(session), int(frame), int(word), ctypes.c_uint32(xor_mask & 0xFFFFFFFF)))
+
+    def profile_enable(self, on: bool = True) -> None:
+        _raise(self._lib, self._h, self._lib.rb_profile_enable(self._h, 1 if on else 0))
+
+    def profile_take(self):
+        """(summed tick-kernel milliseconds, launches) since the last call."""
+        ms = ctypes.c_double()
+        n = ctypes.c_int32()
+        _raise(self._lib, self._h, self._lib.rb_profile_take(self._h, ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+
+# --------------------------------------------------------------------------- decoding helpers
+def decode_ex_game(images: np.ndarray, num_players: int) -> dict:
+    """Split bincode images of ex_game State (ex_game.rs:224-231) into fields."""
+    P = num_players
+    assert images.shape[-1] == 36 + 20 * P
+    out = {"frame": images[..., 0:4].copy().view(np.int32)[..., 0]}
+    out["num_players"] = images[..., 4:12].copy().view(np.uint64)[..., 0]
+    out["positions"] = images[..., 20:20 + 8 * P].copy().view(np.float32).reshape(images.shape[:-1] + (P, 2))
+    o = 28 + 8 * P
+    out["velocities"] = images[..., o:o + 8 * P].copy().view(np.float32).reshape(images.shape[:-1] + (P, 2))
+    o = 36 + 16 * P
+    out["rotations"] = images[..., o:o + 4 * P].copy().view(np.float32)
+    return out

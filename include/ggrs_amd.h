@@ -1,0 +1,176 @@
+/* ===========================================================================
+ * ggrs_amd.h — C ABI of the MI355X batched rollback-resimulation engine.
+ *
+ * Drop-in boundary for the GGRS 0.9.4 resimulation path (/root/reference):
+ * a batch of S lock-step SyncTestSessions whose request stream
+ * (SaveGameState / LoadGameState / AdvanceFrame, lib.rs:170-194) is produced
+ * by host-side bookkeeping identical to the reference and executed on the GPU
+ * by compiled-in game handlers (the user's `handle_requests`, ex_game.rs:76-84).
+ *
+ * Plain C types only (no torch, no HIP types in signatures): a Rust `extern
+ * "C"` block, a ctypes stub or a C++ wrapper binds it directly; see
+ * INTEGRATION.md.  Every entry point names the reference interface it
+ * replaces.
+ *
+ * Threading: one batch = one HIP stream; calls on one batch are not reentrant.
+ * Different batches (e.g. one per GPU) may be driven from different threads.
+ * No exception or panic crosses the ABI: every call returns rb_status.
+ * ======================================================================== */
+#ifndef GGRS_AMD_H
+#define GGRS_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RB_ABI_VERSION 1
+#define RB_NULL_FRAME (-1) /* lib.rs:46 NULL_FRAME */
+#define RB_INPUT_QUEUE_LENGTH 128 /* input_queue.rs:6 */
+
+/* GGRSError (error.rs:11-36) as status codes, plus engine-side failures. */
+typedef enum rb_status {
+  RB_OK = 0,
+  RB_PREDICTION_THRESHOLD = 1,     /* GGRSError::PredictionThreshold          error.rs:13 */
+  RB_INVALID_REQUEST = 2,          /* GGRSError::InvalidRequest{info}         error.rs:15-18 (info: rb_last_error) */
+  RB_MISMATCHED_CHECKSUM = 3,      /* GGRSError::MismatchedChecksum{frame}    error.rs:22-25 (per session: rb_mismatches) */
+  RB_NOT_SYNCHRONIZED = 4,         /* GGRSError::NotSynchronized              error.rs:27 */
+  RB_SPECTATOR_TOO_FAR_BEHIND = 5, /* GGRSError::SpectatorTooFarBehind        error.rs:29 */
+  RB_DEVICE_ERROR = 100,           /* HIP runtime failure (no reference analogue) */
+  RB_PANIC = 101                   /* a reference assert!/panic! condition was hit (API misuse) */
+} rb_status;
+
+/* Compiled-in game handlers (the `Config` trait's State/Input + handle_requests). */
+typedef enum rb_game {
+  RB_GAME_EX_GAME = 1,        /* examples/ex_game/ex_game.rs: f32 ships, Input{inp:u8}, fletcher16 over the bincode image */
+  RB_GAME_STUB = 2,           /* tests/stubs.rs GameStub: i32 state, StubInput{inp:u32}, SipHash-1-3 checksum */
+  RB_GAME_STUB_ENUM = 3,      /* tests/stubs_enum.rs GameStubEnum: #[repr(u8)] enum input */
+  RB_GAME_STUB_RANDOM_CS = 4  /* tests/stubs.rs RandomChecksumGameStub: random u128 checksums (forces mismatches) */
+} rb_game;
+
+/* GGRSRequest kinds (lib.rs:170-194) for rb_last_requests. */
+typedef enum rb_request_kind { RB_REQ_SAVE = 0, RB_REQ_LOAD = 1, RB_REQ_ADVANCE = 2 } rb_request_kind;
+
+#define RB_FLAG_CHECKED 1u /* advance_frame reports MismatchedChecksum synchronously, like the reference (default) */
+
+/* SessionBuilder fields used by start_synctest_session (builder.rs:32-52). */
+typedef struct rb_config {
+  int32_t abi_version;    /* = RB_ABI_VERSION */
+  int32_t game;           /* rb_game */
+  int32_t num_sessions;   /* batch size S (independent sessions in lock-step) */
+  int32_t num_players;    /* with_num_players          builder.rs:154-157 (default 2) */
+  int32_t max_prediction; /* with_max_prediction_window builder.rs:136-145 (default 8, >0, <= 64 here) */
+  int32_t check_distance; /* with_check_distance       builder.rs:202-205 (default 2, < max_prediction) */
+  int32_t input_delay;    /* with_input_delay          builder.rs:148-151 (default 0) */
+  int32_t device;         /* HIP device ordinal; -1 = plan-only batch (host bookkeeping, no device work) */
+  uint64_t seed;          /* RB_GAME_STUB_RANDOM_CS only */
+  uint32_t flags;         /* RB_FLAG_* */
+  uint32_t block_size;    /* 0 = default; kernel tuning knob */
+  uint32_t reserved[6];
+} rb_config;
+
+typedef struct rb_batch rb_batch;
+
+/* Checksum report record (mirrors messages.rs:75-79 ChecksumReport{checksum:u128, frame}
+ * + the session's desync flag) written to device memory by rb_export_checksum_report. */
+typedef struct rb_checksum_report {
+  uint64_t checksum_lo;
+  uint64_t checksum_hi;
+  int32_t frame;
+  int32_t mismatch_frame; /* RB_NULL_FRAME when the session is healthy */
+} rb_checksum_report;
+
+/* SessionBuilder::new() defaults (builder.rs:13-27, 62-78). */
+void rb_config_init(rb_config* cfg);
+
+/* SessionBuilder::start_synctest_session (builder.rs:342-354) for S sessions.
+ * Validation errors as in the reference ("Check distance too big.", zero
+ * prediction window) -> RB_INVALID_REQUEST; *out = NULL and the message via
+ * rb_last_error(NULL). */
+rb_status rb_synctest_create(const rb_config* cfg, rb_batch** out);
+void rb_destroy(rb_batch* b);
+
+/* Last error message of this batch (or of the failed create when b == NULL). */
+const char* rb_last_error(const rb_batch* b);
+
+/* Run this batch on a caller-owned hipStream_t (passed as void*); NULL = the
+ * batch's own stream. */
+rb_status rb_set_stream(rb_batch* b, void* hip_stream);
+
+/* SyncTestSession::add_local_input (sync_test_session.rs:61-74) for every
+ * session at once: `inputs` holds S values of the game's Input type
+ * (ex_game: u8, stub: u32, enum: u8) for player `handle`; host or device
+ * pointer.  Device pointers must stay valid until the next advance has run
+ * (stream order).  Overwrites an earlier call for the same handle.
+ * handle >= num_players -> RB_INVALID_REQUEST. */
+rb_status rb_add_local_input(rb_batch* b, int32_t handle, const void* inputs, int32_t on_device);
+
+/* All players at once, packed [S][num_players] Input values. */
+rb_status rb_add_local_inputs_packed(rb_batch* b, const void* inputs, int32_t on_device);
+
+/* SyncTestSession::advance_frame (sync_test_session.rs:85-146) followed by
+ * the game's handle_requests on every session, fused into one device launch.
+ * Returns RB_INVALID_REQUEST (missing input), RB_PREDICTION_THRESHOLD, or —
+ * with RB_FLAG_CHECKED — RB_MISMATCHED_CHECKSUM when at least one session's
+ * advance_frame returned Err(MismatchedChecksum) in this call.  A session that
+ * failed does not advance (as in the reference, where every retry fails the
+ * same way); the others do.  Without RB_FLAG_CHECKED the call is fully
+ * asynchronous and mismatches are read with rb_mismatches. */
+rb_status rb_advance_frame(rb_batch* b);
+
+/* SyncLayer::current_frame of the batch (sync_layer.rs:110-112). */
+int32_t rb_current_frame(const rb_batch* b);
+int32_t rb_num_sessions(const rb_batch* b);
+/* Bytes of one session's canonical state image (ex_game: the bincode image,
+ * 36+20*P; stubs: le32 frame || le32 state) and of one Input value. */
+int32_t rb_state_bytes(const rb_batch* b);
+int32_t rb_input_bytes(const rb_batch* b);
+
+/* Wait for all work queued on the batch's stream. */
+rb_status rb_synchronize(rb_batch* b);
+
+/* Per-session MismatchedChecksum{frame} (RB_NULL_FRAME when healthy) and the
+ * count of failed sessions.  Synchronises. */
+rb_status rb_mismatches(rb_batch* b, int32_t* frames_out, int32_t* count_out);
+
+/* The (kind, frame) list of the request stream the last rb_advance_frame
+ * executed, identical to the Vec<GGRSRequest> the reference returns
+ * (AdvanceFrame carries the frame it advances from).  Returns the count. */
+int32_t rb_last_requests(const rb_batch* b, int32_t* kinds, int32_t* frames, int32_t cap);
+
+/* GameStateCell::{load, checksum} (sync_layer.rs:28-39) for the cell holding
+ * `frame`: images [S][rb_state_bytes], checksums [S][2] (u128 lo, hi).
+ * RB_INVALID_REQUEST if no cell holds that frame.  Synchronises. */
+rb_status rb_read_cell(rb_batch* b, int32_t frame, void* images, uint64_t* checksums);
+
+/* The game's live state after the last advance (ex_game Game::game_state) and
+ * its display checksum (Game::last_checksum, ex_game.rs:104-111).  Synchronises. */
+rb_status rb_read_live(rb_batch* b, void* images, uint64_t* display_checksums, int32_t* display_frame);
+
+/* Desync report for the cell holding `frame` into device memory [S]
+ * rb_checksum_report (the P2P ChecksumReport payload; multi-GPU allgather
+ * input).  Stream-ordered, does not synchronise. */
+rb_status rb_export_checksum_report(rb_batch* b, int32_t frame, void* dev_out);
+
+/* Fault injection for tests: XOR `xor_mask` into state word `word` of
+ * `session` in the cell holding `frame` (a corrupted snapshot makes the next
+ * resimulation diverge, which SyncTest must report). */
+rb_status rb_debug_corrupt_cell(rb_batch* b, int32_t session, int32_t frame, int32_t word, uint32_t xor_mask);
+
+/* Device evaluation of the game's sin/cos (the glibc sinf/cosf restatement in
+ * device_math.hpp) for n host floats, on `device` — pins it against the host
+ * libm in the parity tests. */
+rb_status rb_debug_sincosf(int32_t device, const float* x, float* sin_out, float* cos_out, int64_t n);
+
+/* HIP event timing of the tick kernel over the batch's stream, for bench.py:
+ * returns the summed milliseconds and the count of tick launches since the
+ * last call, and resets them (requires rb_profile_enable(b, 1) first). */
+rb_status rb_profile_enable(rb_batch* b, int32_t on);
+rb_status rb_profile_take(rb_batch* b, double* total_ms, int32_t* launches);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+#endif /* GGRS_AMD_H */

@@ -1,0 +1,167 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes driver of the CPU restatement (oracle/).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module.  It loads oracle/build/liboracle.so (built by oracle/Makefile)
+and exposes S independent reference sessions (SyncTestSession + game,
+driven like ex_game_synctest.rs:59-72).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+REF_TESTS = os.path.join(_HERE, "build", "ref_tests")
+
+EX_GAME, STUB, STUB_ENUM, STUB_RANDOM_CS = 1, 2, 3, 4
+KIND_PANIC = 99
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} missing: run `make -C oracle`")
+        lib = ctypes.CDLL(LIB_PATH)
+        P, I32, U64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint64
+        PI32 = ctypes.POINTER(ctypes.c_int32)
+        sig = {
+            "orc_image_bytes": (I32, [I32, I32]),
+            "orc_input_bytes": (I32, [I32]),
+            "orc_batch_create": (P, [I32, I32, I32, I32, I32, I32, U64]),
+            "orc_last_error": (ctypes.c_char_p, []),
+            "orc_last_panic": (ctypes.c_char_p, [P]),
+            "orc_batch_destroy": (None, [P]),
+            "orc_batch_add_local_input": (I32, [P, I32, P]),
+            "orc_batch_advance": (I32, [P, PI32, PI32]),
+            "orc_batch_trace": (I32, [P, I32, PI32, PI32, I32]),
+            "orc_batch_read_cells": (I32, [P, PI32, P, P, P]),
+            "orc_batch_read_live": (I32, [P, P, P, PI32]),
+            "orc_batch_current_frame": (I32, [P]),
+            "orc_fletcher16": (ctypes.c_uint16, [P, U64]),
+            "orc_siphash": (U64, [I32, I32, U64, U64, P, U64]),
+            "orc_cosf": (ctypes.c_float, [ctypes.c_float]),
+            "orc_sinf": (ctypes.c_float, [ctypes.c_float]),
+            "orc_sincosf_array": (None, [P, P, P, ctypes.c_int64]),
+            "orc_batch_corrupt_cell": (I32, [P, I32, I32, I32, ctypes.c_uint32]),
+            "orc_synth_inputs": (None, [U64, ctypes.c_uint32, I32, I32, I32, I32, I32, P]),
+            "orc_bench_exgame": (ctypes.c_double, [I32, I32, I32, I32, I32, I32, I32, I32, U64, PI32]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class OracleBatch:
+    """S independent reference sessions of one game (TEST ONLY)."""
+
+    def __init__(self, game: int, num_players: int, max_prediction: int, check_distance: int,
+                 input_delay: int, num_sessions: int, seed: int = 0):
+        lib = load()
+        self._lib = lib
+        self._h = lib.orc_batch_create(game, num_players, max_prediction, check_distance, input_delay,
+                                       num_sessions, seed)
+        if not self._h:
+            raise ValueError(lib.orc_last_error().decode())
+        self.game, self.P, self.W, self.S = game, num_players, max_prediction, num_sessions
+        self.image_bytes = lib.orc_image_bytes(game, num_players)
+        self.input_dtype = np.uint32 if lib.orc_input_bytes(game) == 4 else np.uint8
+
+    def close(self):
+        if self._h:
+            self._lib.orc_batch_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def add_local_input(self, handle: int, inputs) -> int:
+        a = np.ascontiguousarray(np.broadcast_to(np.asarray(inputs), (self.S,)), dtype=self.input_dtype)
+        return self._lib.orc_batch_add_local_input(self._h, handle, _ptr(a))
+
+    def advance(self):
+        """(error kinds [S], error frames [S]); kind 0 = Ok, 3 = MismatchedChecksum, 99 = panic."""
+        k = np.empty(self.S, np.int32)
+        f = np.empty(self.S, np.int32)
+        self._lib.orc_batch_advance(self._h, k.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                    f.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+        return k, f
+
+    def last_panic(self) -> str:
+        return self._lib.orc_last_panic(self._h).decode()
+
+    def trace(self, session: int = 0):
+        cap = 4 * self.W + 8
+        k = (ctypes.c_int32 * cap)()
+        f = (ctypes.c_int32 * cap)()
+        n = self._lib.orc_batch_trace(self._h, session, k, f, cap)
+        return [(k[i], f[i]) for i in range(n)]
+
+    def read_cells(self):
+        """(cell frames [W], images [W, S, B], cs_valid [W, S], checksums [W, S, 2])."""
+        fr = np.empty(self.W, np.int32)
+        img = np.zeros((self.W, self.S, self.image_bytes), np.uint8)
+        val = np.zeros((self.W, self.S), np.uint8)
+        cs = np.zeros((self.W, self.S, 2), np.uint64)
+        self._lib.orc_batch_read_cells(self._h, fr.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), _ptr(img),
+                                       _ptr(val), _ptr(cs))
+        return fr, img, val, cs
+
+    def read_live(self):
+        """(images [S, B], display checksums [S], display frames [S])."""
+        img = np.zeros((self.S, self.image_bytes), np.uint8)
+        cs = np.zeros(self.S, np.uint64)
+        fr = np.zeros(self.S, np.int32)
+        self._lib.orc_batch_read_live(self._h, _ptr(img), _ptr(cs), fr.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+        return img, cs, fr
+
+    def current_frame(self) -> int:
+        return self._lib.orc_batch_current_frame(self._h)
+
+    def corrupt_cell(self, session: int, frame: int, word: int, xor_mask: int) -> None:
+        rc = self._lib.orc_batch_corrupt_cell(self._h, session, frame, word, xor_mask & 0xFFFFFFFF)
+        assert rc == 0, "no cell holds that frame"
+
+
+def fletcher16(data: bytes) -> int:
+    b = np.frombuffer(bytes(data), np.uint8)
+    return load().orc_fletcher16(_ptr(b) if b.size else None, b.size)
+
+
+def siphash(c: int, d: int, k0: int, k1: int, msg: bytes) -> int:
+    b = np.frombuffer(bytes(msg) or b"\0", np.uint8)
+    return load().orc_siphash(c, d, k0, k1, _ptr(b), len(msg))
+
+
+def sincosf(x: np.ndarray):
+    """glibc sinf/cosf of every element (host libm; what Rust's f32::sin/cos call)."""
+    x = np.ascontiguousarray(x, np.float32)
+    s = np.empty_like(x)
+    c = np.empty_like(x)
+    load().orc_sincosf_array(_ptr(x), _ptr(s), _ptr(c), x.size)
+    return s, c
+
+
+def synth_inputs(seed: int, mask: int, S: int, P: int, T: int, f0: int = 0, input_bytes: int = 1) -> np.ndarray:
+    out = np.empty((T, P, S), np.uint8 if input_bytes == 1 else np.uint32)
+    load().orc_synth_inputs(seed, mask, S, P, T, f0, input_bytes, _ptr(out))
+    return out
+
+
+def bench_exgame(num_players: int, check_distance: int, input_delay: int, max_prediction: int, sessions: int,
+                 warmup: int, ticks: int, threads: int, seed: int):
+    """CPU 'port' baseline: wall seconds for `ticks` ticks of `sessions` reference sessions."""
+    ne = ctypes.c_int32()
+    t = load().orc_bench_exgame(num_players, check_distance, input_delay, max_prediction, sessions, warmup, ticks,
+                                threads, seed, ctypes.byref(ne))
+    return t, ne.value

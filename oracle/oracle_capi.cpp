@@ -1,0 +1,340 @@
+// ============================================================================
+// oracle/oracle_capi.cpp — TEST INFRASTRUCTURE ONLY.
+//
+// extern "C" surface of the CPU restatement (oracle/ggrs_oracle.hpp) so that
+// the Python tests (tests/) and bench.py's cpu_baseline leg can drive it via
+// ctypes.  A "batch" here is S fully independent reference sessions, each a
+// SyncTestSession + its game, driven exactly like ex_game_synctest.rs:59-72:
+// add_local_input for every handle, advance_frame, handle_requests.
+// Nothing in the product links this library.
+// ============================================================================
+#include <atomic>
+#include <chrono>
+#include <thread>
+
+#include "ggrs_oracle.hpp"
+
+using namespace orc;
+
+namespace {
+
+enum GameId : int32_t { EX_GAME = 1, STUB = 2, STUB_ENUM = 3, STUB_RANDOM_CS = 4 };
+constexpr int32_t KIND_PANIC = 99;
+
+struct BatchBase {
+  virtual ~BatchBase() = default;
+  virtual int32_t add_local_input(int32_t handle, const uint8_t* inputs) = 0;
+  virtual int32_t advance(int32_t* kinds, int32_t* frames) = 0;
+  virtual int32_t trace(int32_t session, int32_t* kinds, int32_t* frames, int32_t cap) = 0;
+  virtual int32_t read_cells(int32_t* cell_frames, uint8_t* images, uint8_t* cs_valid, uint64_t* cs) = 0;
+  virtual int32_t read_live(uint8_t* images, uint64_t* last_cs, int32_t* last_cs_frame) = 0;
+  virtual int32_t current_frame() = 0;
+  virtual int32_t corrupt_cell(int32_t session, int32_t frame, int32_t word, uint32_t xor_mask) = 0;
+  std::string last_panic;
+};
+
+// Canonical state images: bincode image for ex_game, le32(frame)||le32(state) for stubs.
+inline std::vector<uint8_t> image_of(const exgame::State& s) { return exgame::bincode_serialize(s); }
+inline std::vector<uint8_t> image_of(const stub::StateStub& s) {
+  std::vector<uint8_t> v(8);
+  std::memcpy(v.data(), &s.frame, 4);
+  std::memcpy(v.data() + 4, &s.state, 4);
+  return v;
+}
+inline std::vector<uint8_t> image_of(const stub::StateStubEnum& s) {
+  std::vector<uint8_t> v(8);
+  std::memcpy(v.data(), &s.frame, 4);
+  std::memcpy(v.data() + 4, &s.state, 4);
+  return v;
+}
+inline uint64_t display_checksum(const exgame::Game& g, int32_t* f) { *f = g.last_checksum.first; return g.last_checksum.second; }
+template <class G>
+inline uint64_t display_checksum(const G&, int32_t* f) { *f = NULL_FRAME; return 0; }
+inline const exgame::State& live_of(const exgame::Game& g) { return g.game_state; }
+// Word k of the engine's state layout (positions, velocities, rotations /
+// stub state) flipped in place: fault injection for the desync tests.
+inline void corrupt_state(exgame::State& st, int32_t k, uint32_t m) {
+  const int32_t P = static_cast<int32_t>(st.num_players);
+  float* f;
+  if (k < 2 * P) f = (k % 2) ? &st.positions[k / 2].second : &st.positions[k / 2].first;
+  else if (k < 4 * P) f = ((k - 2 * P) % 2) ? &st.velocities[(k - 2 * P) / 2].second : &st.velocities[(k - 2 * P) / 2].first;
+  else f = &st.rotations[k - 4 * P];
+  uint32_t u;
+  std::memcpy(&u, f, 4);
+  u ^= m;
+  std::memcpy(f, &u, 4);
+}
+inline void corrupt_state(stub::StateStub& st, int32_t, uint32_t m) { st.state ^= static_cast<int32_t>(m); }
+inline void corrupt_state(stub::StateStubEnum& st, int32_t, uint32_t m) { st.state ^= static_cast<int32_t>(m); }
+template <class G>
+inline const auto& live_of(const G& g) { return g.gs; }
+
+template <class C, class G>
+struct Batch : BatchBase {
+  using I = typename C::Input;
+  std::vector<std::unique_ptr<SyncTestSession<C>>> sess;
+  std::vector<G> games;
+  std::vector<std::vector<Request<C>>> last_reqs;
+  size_t max_pred;
+
+  template <class MakeGame>
+  Batch(const SessionBuilder& b, int32_t S, MakeGame mk) : max_pred(b.max_prediction) {
+    for (int32_t s = 0; s < S; ++s) {
+      std::unique_ptr<SyncTestSession<C>> p;
+      Error e = b.start_synctest_session<C>(&p);
+      if (e.is_err()) throw std::runtime_error(e.info);
+      sess.push_back(std::move(p));
+      games.push_back(mk(s));
+    }
+    last_reqs.resize(S);
+  }
+
+  int32_t add_local_input(int32_t handle, const uint8_t* in) override {
+    int32_t first = 0;
+    for (size_t s = 0; s < sess.size(); ++s) {
+      I v{};
+      std::memcpy(&v, in + s * sizeof(I), sizeof(I));
+      Error e = sess[s]->add_local_input(static_cast<PlayerHandle>(handle < 0 ? SIZE_MAX : handle), v);
+      if (e.is_err() && first == 0) first = static_cast<int32_t>(e.kind);
+    }
+    return first;
+  }
+
+  int32_t advance(int32_t* kinds, int32_t* frames) override {
+    int32_t nerr = 0;
+    for (size_t s = 0; s < sess.size(); ++s) {
+      int32_t k = 0;
+      Frame f = NULL_FRAME;
+      try {
+        Error e = sess[s]->advance_frame(last_reqs[s]);
+        if (e.is_err()) {
+          k = static_cast<int32_t>(e.kind);
+          f = e.frame;
+          last_reqs[s].clear();
+        } else {
+          games[s].handle_requests(last_reqs[s]);
+        }
+      } catch (const Panic& p) {
+        k = KIND_PANIC;
+        last_panic = p.what();
+      }
+      if (k) ++nerr;
+      if (kinds) kinds[s] = k;
+      if (frames) frames[s] = f;
+    }
+    return nerr;
+  }
+
+  int32_t trace(int32_t session, int32_t* kinds, int32_t* frames, int32_t cap) override {
+    auto& r = last_reqs.at(session);
+    int32_t n = static_cast<int32_t>(r.size());
+    for (int32_t i = 0; i < n && i < cap; ++i) {
+      kinds[i] = static_cast<int32_t>(r[i].kind);
+      frames[i] = r[i].frame;
+    }
+    return n;
+  }
+
+  int32_t read_cells(int32_t* cell_frames, uint8_t* images, uint8_t* cs_valid, uint64_t* cs) override {
+    const size_t S = sess.size();
+    size_t img = 0;
+    for (size_t w = 0; w < max_pred; ++w) {
+      for (size_t s = 0; s < S; ++s) {
+        const auto& cell = sess[s]->sync_layer.saved_states.states[w];
+        if (s == 0 && cell_frames) cell_frames[w] = cell.frame();
+        auto d = cell.load();
+        if (d) {
+          auto v = image_of(*d);
+          img = v.size();
+          if (images) std::memcpy(images + (w * S + s) * img, v.data(), img);
+        }
+        auto c = cell.checksum();
+        if (cs_valid) cs_valid[w * S + s] = c.has_value();
+        if (cs) {
+          u128 x = c.value_or(0);
+          cs[(w * S + s) * 2 + 0] = static_cast<uint64_t>(x);
+          cs[(w * S + s) * 2 + 1] = static_cast<uint64_t>(x >> 64);
+        }
+      }
+    }
+    return static_cast<int32_t>(img);
+  }
+
+  int32_t read_live(uint8_t* images, uint64_t* last_cs, int32_t* last_cs_frame) override {
+    size_t img = 0;
+    for (size_t s = 0; s < sess.size(); ++s) {
+      auto v = image_of(live_of(games[s]));
+      img = v.size();
+      if (images) std::memcpy(images + s * img, v.data(), img);
+      int32_t f;
+      uint64_t c = display_checksum(games[s], &f);
+      if (last_cs) last_cs[s] = c;
+      if (last_cs_frame) last_cs_frame[s] = f;
+    }
+    return static_cast<int32_t>(img);
+  }
+
+  int32_t current_frame() override { return sess.empty() ? 0 : sess[0]->current_frame(); }
+
+  int32_t corrupt_cell(int32_t session, int32_t frame, int32_t word, uint32_t m) override {
+    auto cell = sess.at(session)->sync_layer.saved_state_by_frame(frame);
+    if (!cell) return -1;
+    auto d = cell->load();
+    if (!d) return -1;
+    corrupt_state(*d, word, m);
+    cell->save(frame, *d, cell->checksum());
+    return 0;
+  }
+};
+
+thread_local std::string g_err;
+
+}  // namespace
+
+extern "C" {
+
+int32_t orc_image_bytes(int32_t game, int32_t num_players) {
+  return game == EX_GAME ? 36 + 20 * num_players : 8;
+}
+int32_t orc_input_bytes(int32_t game) { return (game == STUB || game == STUB_RANDOM_CS) ? 4 : 1; }
+
+// Returns NULL on a builder error (message via orc_last_error).
+void* orc_batch_create(int32_t game, int32_t num_players, int32_t max_prediction, int32_t check_distance,
+                       int32_t input_delay, int32_t num_sessions, uint64_t seed) {
+  try {
+    SessionBuilder b;
+    b.with_num_players(num_players).with_check_distance(check_distance).with_input_delay(input_delay);
+    Error e = b.with_max_prediction_window(static_cast<size_t>(max_prediction));
+    if (e.is_err()) { g_err = e.info; return nullptr; }
+    switch (game) {
+      case EX_GAME:
+        return new Batch<exgame::Config, exgame::Game>(b, num_sessions, [&](int32_t) { return exgame::Game(num_players); });
+      case STUB:
+        return new Batch<stub::Config, stub::GameStub>(b, num_sessions, [&](int32_t) { return stub::GameStub{}; });
+      case STUB_ENUM:
+        return new Batch<stub::EnumConfig, stub::GameStubEnum>(b, num_sessions, [&](int32_t) { return stub::GameStubEnum{}; });
+      case STUB_RANDOM_CS:
+        return new Batch<stub::Config, stub::RandomChecksumGameStub>(
+            b, num_sessions, [&](int32_t s) { return stub::RandomChecksumGameStub(seed ^ (uint64_t(s) * 0x9e37ULL)); });
+      default: g_err = "unknown game"; return nullptr;
+    }
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return nullptr;
+  }
+}
+const char* orc_last_error() { return g_err.c_str(); }
+const char* orc_last_panic(void* b) { return static_cast<BatchBase*>(b)->last_panic.c_str(); }
+void orc_batch_destroy(void* b) { delete static_cast<BatchBase*>(b); }
+int32_t orc_batch_add_local_input(void* b, int32_t handle, const uint8_t* inputs) {
+  return static_cast<BatchBase*>(b)->add_local_input(handle, inputs);
+}
+int32_t orc_batch_advance(void* b, int32_t* kinds, int32_t* frames) {
+  return static_cast<BatchBase*>(b)->advance(kinds, frames);
+}
+int32_t orc_batch_trace(void* b, int32_t session, int32_t* kinds, int32_t* frames, int32_t cap) {
+  return static_cast<BatchBase*>(b)->trace(session, kinds, frames, cap);
+}
+int32_t orc_batch_read_cells(void* b, int32_t* cell_frames, uint8_t* images, uint8_t* cs_valid, uint64_t* cs) {
+  return static_cast<BatchBase*>(b)->read_cells(cell_frames, images, cs_valid, cs);
+}
+int32_t orc_batch_read_live(void* b, uint8_t* images, uint64_t* last_cs, int32_t* last_cs_frame) {
+  return static_cast<BatchBase*>(b)->read_live(images, last_cs, last_cs_frame);
+}
+int32_t orc_batch_current_frame(void* b) { return static_cast<BatchBase*>(b)->current_frame(); }
+
+// Third-party arithmetic, exposed for the known-answer tests.
+uint16_t orc_fletcher16(const uint8_t* d, uint64_t n) { return fletcher16(d, n); }
+uint64_t orc_siphash(int32_t c, int32_t d, uint64_t k0, uint64_t k1, const uint8_t* m, uint64_t n) {
+  return siphash(c, d, k0, k1, m, n);
+}
+float orc_cosf(float x) { return std::cos(x); }
+float orc_sinf(float x) { return std::sin(x); }
+void orc_sincosf_array(const float* in, float* s, float* c, int64_t n) {
+  for (int64_t i = 0; i < n; ++i) {
+    s[i] = std::sin(in[i]);
+    c[i] = std::cos(in[i]);
+  }
+}
+int32_t orc_batch_corrupt_cell(void* b, int32_t session, int32_t frame, int32_t word, uint32_t m) {
+  return static_cast<BatchBase*>(b)->corrupt_cell(session, frame, word, m);
+}
+// Synthetic inputs [T][P][S] (u8 or u32 per input_bytes), see ggrs_oracle.hpp SynthInput.
+void orc_synth_inputs(uint64_t seed, uint32_t mask, int32_t S, int32_t P, int32_t T, int32_t f0, int32_t input_bytes,
+                      void* out) {
+  SynthInput g{seed, mask};
+  std::vector<uint32_t> prev(static_cast<size_t>(S) * P, 0);
+  // replay the hold model from frame 0 up to f0 first
+  for (int32_t f = 0; f < f0 + T; ++f)
+    for (int32_t p = 0; p < P; ++p)
+      for (int32_t s = 0; s < S; ++s) {
+        uint32_t& v = prev[static_cast<size_t>(p) * S + s];
+        v = g.next(v, s, p, f);
+        if (f >= f0) {
+          size_t idx = (static_cast<size_t>(f - f0) * P + p) * S + s;
+          if (input_bytes == 1) static_cast<uint8_t*>(out)[idx] = static_cast<uint8_t>(v);
+          else static_cast<uint32_t*>(out)[idx] = v;
+        }
+      }
+}
+
+// CPU baseline ("port"): S independent ex_game SyncTest sessions driven exactly
+// like ex_game_synctest.rs:59-72 on `threads` host threads.  Inputs are
+// generated before the timed region (as on the GPU side).  Returns the wall
+// seconds of the `ticks` timed ticks (after `warmup` untimed ones); writes the
+// number of sessions that reported an error to *n_err.
+double orc_bench_exgame(int32_t num_players, int32_t check_distance, int32_t input_delay, int32_t max_prediction,
+                        int32_t S, int32_t warmup, int32_t ticks, int32_t threads, uint64_t seed, int32_t* n_err) {
+  SessionBuilder b;
+  b.with_num_players(num_players).with_check_distance(check_distance).with_input_delay(input_delay);
+  if (b.with_max_prediction_window(max_prediction).is_err()) return -1.0;
+  const int32_t P = num_players, T = warmup + ticks;
+  std::vector<uint8_t> in(static_cast<size_t>(T) * P * S);
+  orc_synth_inputs(seed, 0x0F, S, P, T, 0, 1, in.data());
+  if (threads < 1) threads = 1;
+  struct Worker {
+    std::vector<std::unique_ptr<SyncTestSession<exgame::Config>>> sess;
+    std::vector<exgame::Game> games;
+    int32_t s0 = 0, s1 = 0, errs = 0;
+  };
+  std::vector<Worker> ws(threads);
+  for (int32_t t = 0; t < threads; ++t) {
+    ws[t].s0 = static_cast<int32_t>(static_cast<int64_t>(S) * t / threads);
+    ws[t].s1 = static_cast<int32_t>(static_cast<int64_t>(S) * (t + 1) / threads);
+  }
+  auto run = [&](Worker& w, int32_t f0, int32_t f1) {
+    std::vector<Request<exgame::Config>> reqs;
+    for (int32_t f = f0; f < f1; ++f)
+      for (int32_t s = w.s0; s < w.s1; ++s) {
+        auto& sess = *w.sess[s - w.s0];
+        for (int32_t p = 0; p < P; ++p)
+          sess.add_local_input(p, exgame::Input{in[(static_cast<size_t>(f) * P + p) * S + s]});
+        Error e = sess.advance_frame(reqs);
+        if (e.is_err()) { ++w.errs; continue; }
+        w.games[s - w.s0].handle_requests(reqs);
+      }
+  };
+  auto parallel = [&](auto fn) {
+    std::vector<std::thread> th;
+    for (int32_t t = 0; t < threads; ++t) th.emplace_back([&, t] { fn(ws[t]); });
+    for (auto& x : th) x.join();
+  };
+  parallel([&](Worker& w) {
+    for (int32_t s = w.s0; s < w.s1; ++s) {
+      std::unique_ptr<SyncTestSession<exgame::Config>> p;
+      b.start_synctest_session<exgame::Config>(&p);
+      w.sess.push_back(std::move(p));
+      w.games.emplace_back(num_players);
+    }
+    run(w, 0, warmup);
+  });
+  auto t0 = std::chrono::steady_clock::now();
+  parallel([&](Worker& w) { run(w, warmup, T); });
+  auto t1 = std::chrono::steady_clock::now();
+  int32_t e = 0;
+  for (auto& w : ws) e += w.errs;
+  if (n_err) *n_err = e;
+  return std::chrono::duration<double>(t1 - t0).count();
+}
+
+}  // extern "C"

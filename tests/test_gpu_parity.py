@@ -1,0 +1,275 @@
+"""GPU parity: the HIP engine (through the C ABI) against the CPU oracle.
+
+Bar (BASELINE.json north_star): frame indices and request streams identical;
+integer-state checksums bit-exact; ex_game f32 state within 1e-5 relative.
+The engine restates glibc's sinf/cosf exactly (ggrs_amd/csrc/device_math.hpp),
+so ex_game is asserted BIT-EXACT here too (state images and fletcher16
+checksums), which implies the 1e-5 relative tolerance (asserted as well).
+"""
+import numpy as np
+import pytest
+
+import ggrs_amd as G
+from ggrs_amd.synth import synth_inputs
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+F32_RTOL = 1e-5  # north_star tolerance for f32 ex_game state
+
+ORC_GAME = {G.Game.EX_GAME: O.EX_GAME, G.Game.STUB: O.STUB, G.Game.STUB_ENUM: O.STUB_ENUM,
+            G.Game.STUB_RANDOM_CS: O.STUB_RANDOM_CS}
+
+
+def make_pair(game, S, P=2, W=8, cd=2, d=0, checked=True, seed=0):
+    sess = (G.SessionBuilder(game, num_sessions=S).with_num_players(P).with_max_prediction_window(W)
+            .with_check_distance(cd).with_input_delay(d).with_checked_mismatches(checked).with_seed(seed)
+            .start_synctest_session())
+    orc = O.OracleBatch(ORC_GAME[game], P, W, cd, d, S, seed)
+    return sess, orc
+
+
+def compare_cells(sess, orc, P, game):
+    frames, imgs, valid, cs = orc.read_cells()
+    for w, fr in enumerate(frames):
+        if fr < 0:
+            continue
+        gimg, gcs = sess.read_cell(int(fr))
+        np.testing.assert_array_equal(gimg, imgs[w], err_msg=f"cell image frame {fr}")
+        assert valid[w].all()
+        np.testing.assert_array_equal(gcs, cs[w], err_msg=f"cell checksum frame {fr}")
+        if game == G.Game.EX_GAME:
+            a = G.decode_ex_game(gimg, P)
+            b = G.decode_ex_game(imgs[w], P)
+            for key in ("positions", "velocities", "rotations"):
+                np.testing.assert_allclose(a[key], b[key], rtol=F32_RTOL, atol=0)
+
+
+def compare_live(sess, orc, game):
+    gimg, gdcs, gfr = sess.read_live()
+    oimg, odcs, ofr = orc.read_live()
+    np.testing.assert_array_equal(gimg, oimg, err_msg="live state")
+    if game == G.Game.EX_GAME:
+        np.testing.assert_array_equal(gdcs, odcs, err_msg="display checksum (Game::last_checksum)")
+        assert (ofr == gfr).all()
+
+
+def run_parity(game, S, P, W, cd, d, T, inputs, check_every=1, checked=True):
+    sess, orc = make_pair(game, S, P, W, cd, d, checked)
+    for t in range(T):
+        for h in range(P):
+            sess.add_local_input(h, inputs[t, h])
+            orc.add_local_input(h, inputs[t, h])
+        reqs = sess.advance_frame()
+        kinds, frames = orc.advance()
+        assert (kinds == 0).all(), (t, kinds[:4], orc.last_panic())
+        assert [(int(r.kind), r.frame) for r in reqs] == orc.trace(0), t
+        if t % check_every == 0 or t == T - 1:
+            compare_cells(sess, orc, P, game)
+            compare_live(sess, orc, game)
+    assert (sess.mismatches() == G.NULL_FRAME).all()
+    sess.close()
+
+
+# ---------------------------------------------------------------------------- device math
+def test_device_sincosf_bit_exact_with_glibc(gpu_available):
+    import ctypes
+    from ggrs_amd import _lib as L
+    lo = np.float32(-0.1).view(np.uint32)
+    hi = np.float32(6.4).view(np.uint32)
+    pos = np.arange(0, hi, 37, dtype=np.uint32)  # every 37th float in [0, 6.4]
+    neg = np.arange(0x80000000, lo, 37, dtype=np.uint32)  # [-0.1, -0]
+    special = np.array([0.0, 2 * np.pi, np.pi, np.pi / 2, np.pi / 4, float.fromhex("0x1.921FB6p-1"), 1e-30, 6.2831855, 119.9],
+                       np.float32).view(np.uint32)
+    x = np.concatenate([pos, neg, special]).view(np.float32)
+    gs = np.empty_like(x)
+    gc = np.empty_like(x)
+    st = L.load().rb_debug_sincosf(0, x.ctypes.data_as(ctypes.c_void_p), gs.ctypes.data_as(ctypes.c_void_p),
+                                   gc.ctypes.data_as(ctypes.c_void_p), x.size)
+    assert st == 0
+    hs, hc = O.sincosf(x)
+    bad_s = np.nonzero(gs.view(np.uint32) != hs.view(np.uint32))[0]
+    bad_c = np.nonzero(gc.view(np.uint32) != hc.view(np.uint32))[0]
+    assert bad_s.size == 0, (x[bad_s[:5]], gs[bad_s[:5]], hs[bad_s[:5]])
+    assert bad_c.size == 0, (x[bad_c[:5]], gc[bad_c[:5]], hc[bad_c[:5]])
+
+
+# ---------------------------------------------------------------------------- ex_game
+@pytest.mark.parametrize("P,W,cd,d", [(2, 8, 7, 2), (2, 8, 2, 0), (2, 8, 0, 0), (2, 8, 1, 0), (1, 8, 3, 1),
+                                      (3, 8, 5, 2), (4, 8, 7, 2), (2, 9, 8, 0), (2, 16, 12, 3)])
+def test_exgame_parity_every_tick(gpu_available, P, W, cd, d):
+    S, T = 200, 70
+    inputs = synth_inputs(S, P, T)
+    run_parity(G.Game.EX_GAME, S, P, W, cd, d, T, inputs)
+
+
+def test_exgame_parity_long_run_periodic_and_wraparound(gpu_available):
+    # > 128 frames wraps the input queue ring; frame 100/200 hit CHECKSUM_PERIOD.
+    S, P, T = 130, 2, 260
+    inputs = synth_inputs(S, P, T, seed=12345)
+    run_parity(G.Game.EX_GAME, S, P, 8, 7, 2, T, inputs, check_every=37)
+
+
+def test_exgame_unchecked_mode_same_results(gpu_available):
+    S, P, T = 96, 2, 40
+    inputs = synth_inputs(S, P, T, seed=99)
+    run_parity(G.Game.EX_GAME, S, P, 8, 7, 2, T, inputs, check_every=13, checked=False)
+
+
+def test_exgame_device_and_packed_inputs(gpu_available):
+    import torch
+    S, P, T = 128, 2, 30
+    inputs = synth_inputs(S, P, T, seed=5)
+    a, _ = make_pair(G.Game.EX_GAME, S, P, 8, 7, 2)
+    b, orc = make_pair(G.Game.EX_GAME, S, P, 8, 7, 2)
+    dev = torch.from_numpy(inputs).cuda()  # [T, P, S]
+    packed = torch.from_numpy(np.ascontiguousarray(inputs.transpose(0, 2, 1))).cuda()  # [T, S, P]
+    for t in range(T):
+        for h in range(P):
+            a.add_local_input(h, dev[t, h])
+            orc.add_local_input(h, inputs[t, h])
+        b.add_local_inputs(packed[t])
+        a.advance_frame()
+        b.advance_frame()
+        orc.advance()
+    compare_live(a, orc, G.Game.EX_GAME)
+    compare_live(b, orc, G.Game.EX_GAME)
+    compare_cells(b, orc, P, G.Game.EX_GAME)
+
+
+# ---------------------------------------------------------------------------- integer stubs: bit-exact checksums
+@pytest.mark.parametrize("cd,d", [(0, 0), (2, 0), (7, 2), (3, 5)])
+def test_stub_parity_reference_inputs(gpu_available, cd, d):
+    # tests/test_synctest_session.rs drive both handles with input i at tick i.
+    S, T = 70, 200
+    inputs = np.broadcast_to(np.arange(T, dtype=np.uint32)[:, None, None], (T, 2, S)).copy()
+    run_parity(G.Game.STUB, S, 2, 8, cd, d, T, inputs, check_every=17)
+
+
+def test_stub_parity_random_inputs(gpu_available):
+    S, T = 300, 90
+    inputs = synth_inputs(S, 2, T, mask=0xFFFFFFFF, dtype=np.uint32, seed=3)
+    run_parity(G.Game.STUB, S, 2, 8, 7, 2, T, inputs, check_every=9)
+
+
+def test_stub_enum_parity(gpu_available):
+    # tests/test_synctest_session_enum.rs: alternating Val1/Val2 for both handles,
+    # plus per-session random enum values.
+    S, T = 64, 200
+    alt = np.broadcast_to((np.arange(T) % 2).astype(np.uint8)[:, None, None], (T, 2, S)).copy()
+    run_parity(G.Game.STUB_ENUM, S, 2, 8, 7, 2, T, alt, check_every=50)
+    rnd = synth_inputs(S, 2, 60, mask=1, seed=8)
+    run_parity(G.Game.STUB_ENUM, S, 2, 8, 7, 2, 60, rnd, check_every=7)
+
+
+# ---------------------------------------------------------------------------- mismatch detection
+def test_random_checksums_raise_mismatched_checksum(gpu_available):
+    # tests/test_synctest_session.rs:87-103 (#[should_panic] on the unwrap).
+    S = 50
+    sess, orc = make_pair(G.Game.STUB_RANDOM_CS, S, 2, 8, 2, 2, seed=11)
+    raised_at = None
+    for i in range(12):
+        for h in range(2):
+            sess.add_local_input(h, i)
+            orc.add_local_input(h, i)
+        kinds, frames = orc.advance()
+        try:
+            sess.advance_frame()
+            assert (kinds == 0).all(), i
+        except G.MismatchedChecksum as e:
+            raised_at = raised_at if raised_at is not None else i
+            assert (kinds == 3).all()
+            np.testing.assert_array_equal(e.frames, frames)  # same frame per session (2)
+    assert raised_at == 4
+    # failed sessions keep failing the same way and stop advancing
+    img, _, _ = sess.read_live()
+    oimg, _, _ = orc.read_live()
+    np.testing.assert_array_equal(img, oimg)
+
+
+@pytest.mark.parametrize("game,P,word,mask", [(G.Game.EX_GAME, 2, 0, 0x00000100), (G.Game.EX_GAME, 2, 9, 0x1),
+                                              (G.Game.STUB, 2, 0, 0x4)])
+def test_corrupted_snapshot_detected_like_oracle(gpu_available, game, P, word, mask):
+    S, cd, T = 64, 7, 40
+    dtype = np.uint32 if game == G.Game.STUB else np.uint8
+    inputs = synth_inputs(S, P, T, seed=21, mask=0xFF if game == G.Game.STUB else 0x0F, dtype=dtype)
+    sess, orc = make_pair(game, S, P, 8, cd, 2)
+    victims = [3, 40]
+    for t in range(T):
+        if t == 15:
+            # the cell loaded by the next tick: frame (current - cd)
+            f = sess.current_frame() - cd
+            for v in victims:
+                sess.debug_corrupt_cell(v, f, word, mask)
+                orc.corrupt_cell(v, f, word, mask)
+        for h in range(P):
+            sess.add_local_input(h, inputs[t, h])
+            orc.add_local_input(h, inputs[t, h])
+        kinds, frames = orc.advance()
+        if (kinds != 0).any():
+            with pytest.raises(G.MismatchedChecksum) as ei:
+                sess.advance_frame()
+            np.testing.assert_array_equal(ei.value.frames, np.where(kinds == 3, frames, -1))
+        else:
+            sess.advance_frame()
+    bad = np.nonzero(sess.mismatches() != -1)[0]
+    assert list(bad) == victims
+    compare_live(sess, orc, game)
+
+
+# ---------------------------------------------------------------------------- desync report export
+def test_checksum_report_export(gpu_available):
+    import torch
+    S = 100
+    sess, orc = make_pair(G.Game.EX_GAME, S, 2, 8, 7, 2)
+    inputs = synth_inputs(S, 2, 20)
+    for t in range(20):
+        for h in range(2):
+            sess.add_local_input(h, inputs[t, h])
+        sess.advance_frame()
+    f = sess.current_frame() - 1
+    out = torch.zeros((S, 3), dtype=torch.int64, device="cuda")  # 24-byte rb_checksum_report
+    sess.export_checksum_report(f, out.data_ptr())
+    sess.synchronize()
+    rep = out.cpu().numpy().view(np.uint64)
+    _, cs = sess.read_cell(f)
+    np.testing.assert_array_equal(rep[:, 0], cs[:, 0])
+    np.testing.assert_array_equal(rep[:, 1], cs[:, 1])
+    fr = rep[:, 2].view(np.int32).reshape(S, 2)
+    assert (fr[:, 0] == f).all() and (fr[:, 1] == -1).all()
+
+
+# ---------------------------------------------------------------------------- bench-size properties
+def test_bench_config_65536_sessions_sampled_parity(gpu_available):
+    """BASELINE config 2 at full size: 65,536 ex_game sessions, cd=7, delay 2.
+    Properties at full size: no session reports a mismatch (the resimulation is
+    deterministic) and every tick's stream matches; a sample of sessions is
+    compared bit-exactly with the oracle run on the same per-session inputs."""
+    import torch
+    S, P, T = 65536, 2, 48
+    inputs = synth_inputs(S, P, T)
+    sess = (G.SessionBuilder(G.Game.EX_GAME, num_sessions=S).with_num_players(P).with_check_distance(7)
+            .with_input_delay(2).with_checked_mismatches(False).start_synctest_session())
+    dev = torch.from_numpy(inputs).cuda()
+    for t in range(T):
+        for h in range(P):
+            sess.add_local_input(h, dev[t, h])
+        sess.advance_frame()
+    assert (sess.mismatches() == -1).all()
+    rng = np.random.default_rng(0)
+    sample = np.sort(rng.choice(S, 64, replace=False))
+    orc = O.OracleBatch(O.EX_GAME, P, 8, 7, 2, sample.size)
+    for t in range(T):
+        for h in range(P):
+            orc.add_local_input(h, inputs[t, h, sample])
+        k, _ = orc.advance()
+        assert (k == 0).all()
+    gimg, gdcs, _ = sess.read_live()
+    oimg, odcs, _ = orc.read_live()
+    np.testing.assert_array_equal(gimg[sample], oimg)
+    np.testing.assert_array_equal(gdcs[sample], odcs)
+    frames, oc, _, ocs = orc.read_cells()
+    for w, fr in enumerate(frames):
+        gi, gc = sess.read_cell(int(fr))
+        np.testing.assert_array_equal(gi[sample], oc[w])
+        np.testing.assert_array_equal(gc[sample], ocs[w])
