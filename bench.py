@@ -116,19 +116,24 @@ def main():
     gathered = torch.zeros((S * world, 3), dtype=torch.int64, device=dev) if world > 1 else None
     desyncs = torch.zeros((), dtype=torch.int64, device=dev)
 
-    def tick(t):
-        for h in range(P):
-            sess.add_local_input(h, dinputs[t, h])
-        sess.advance_frame()
-        if world > 1 and args.report_interval and sess.current_frame() % args.report_interval == 0:
-            f = sess.current_frame() - 1
-            sess.export_checksum_report(f, reports.data_ptr())
-            dist.all_gather_into_tensor(gathered, reports)  # RCCL allgather of desync reports
-            desyncs.add_(((gathered[:, 2] >> 32) != -1).sum())  # mismatch_frame != NULL_FRAME
+    def run(t0, t1):
+        """Ticks [t0, t1): native multi-tick calls between desync-report points."""
+        t = t0
+        while t < t1:
+            n = t1 - t
+            if world > 1 and args.report_interval:
+                to_report = args.report_interval - sess.current_frame() % args.report_interval
+                n = min(n, to_report)
+            sess.run_ticks(dinputs[t:t + n])
+            t += n
+            if world > 1 and args.report_interval and sess.current_frame() % args.report_interval == 0:
+                f = sess.current_frame() - 1
+                sess.export_checksum_report(f, reports.data_ptr())
+                dist.all_gather_into_tensor(gathered, reports)  # RCCL allgather of desync reports
+                desyncs.add_(((gathered[:, 2] >> 32) != -1).sum())  # mismatch_frame != NULL_FRAME
 
     with torch.cuda.stream(stream):
-        for t in range(args.warmup):
-            tick(t)
+        run(0, args.warmup)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -136,8 +141,7 @@ def main():
         sess.profile_enable(True)
         sess.profile_take()
         t0 = time.perf_counter()
-        for t in range(args.warmup, T):
-            tick(t)
+        run(args.warmup, T)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()

@@ -74,6 +74,7 @@ SIGNATURES = [
     ("rb_add_local_input", _I32, [_P, _I32, _P, _I32]),
     ("rb_add_local_inputs_packed", _I32, [_P, _P, _I32]),
     ("rb_advance_frame", _I32, [_P]),
+    ("rb_run_ticks", _I32, [_P, _I32, _P, ctypes.c_int64, _I32, _PI32]),
     ("rb_current_frame", _I32, [_P]),
     ("rb_num_sessions", _I32, [_P]),
     ("rb_state_bytes", _I32, [_P]),

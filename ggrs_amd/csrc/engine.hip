@@ -44,6 +44,7 @@ struct KParams {
   void* last_cs;
   void* periodic_cs;
   int32_t* err;
+  int32_t* live_frame;
   unsigned long long* frozen;
   uint32_t* counters;  // [0] sessions failed, [1] unexpected-path count
   const void* in_ptr[4];
@@ -54,6 +55,7 @@ struct KParams {
   int32_t load_slot;  // -1: start from the live state
   int32_t f0, n_steps;
   uint32_t save_modes[kMaxSteps / 16];  // 2 bits per step
+  int32_t slot0;                        // f0 % W (snapshot slot of step 0)
   int32_t live_out, periodic_step, display;
   uint32_t disc_mask;
   uint64_t seed;
@@ -106,71 +108,117 @@ inline size_t word_index(int NW, int Spad, int s, int k) {
   return b + s;
 }
 
-template <class G>
-__device__ __forceinline__ typename G::InRec gather_new_input(const KParams& p, int s) {
+// New inputs of this tick.  kPacked: one [S][P] array; else one [S] array per
+// handle.  The host always passes valid pointers (a dummy when there is no new
+// input), so the loads are unconditional and issue with the others.
+template <class G, bool kPacked>
+__device__ __forceinline__ typename G::InRec gather_new_input(const KParams& p, unsigned s) {
   using InRec = typename G::InRec;
   constexpr int P = G::kPlayers, IB = G::kInputBytes;
-  if (p.in_mode == 2 && sizeof(InRec) == P * IB) return reinterpret_cast<const InRec*>(p.in_ptr[0])[s];
-  uint64_t v = 0;
+  if constexpr (kPacked && sizeof(InRec) == P * IB) {
+    return reinterpret_cast<const InRec*>(p.in_ptr[0])[s];
+  } else {
+    uint64_t v = 0;
 #pragma unroll
-  for (int q = 0; q < P; ++q) {
-    uint64_t x;
-    if (p.in_mode == 2) {
-      const uint8_t* b = reinterpret_cast<const uint8_t*>(p.in_ptr[0]) + (static_cast<size_t>(s) * P + q) * IB;
-      x = 0;
-      for (int i = 0; i < IB; ++i) x |= static_cast<uint64_t>(b[i]) << (8 * i);
-    } else if constexpr (IB == 4) {
-      x = reinterpret_cast<const uint32_t*>(p.in_ptr[q])[s];
-    } else {
-      x = reinterpret_cast<const uint8_t*>(p.in_ptr[q])[s];
+    for (int q = 0; q < P; ++q) {
+      uint64_t x = 0;
+      if constexpr (kPacked) {
+        const uint8_t* b = reinterpret_cast<const uint8_t*>(p.in_ptr[0]) + (s * P + q) * IB;
+#pragma unroll
+        for (int i = 0; i < IB; ++i) x |= static_cast<uint64_t>(b[i]) << (8 * i);
+      } else if constexpr (IB == 4) {
+        x = reinterpret_cast<const uint32_t*>(p.in_ptr[q])[s];
+      } else {
+        x = reinterpret_cast<const uint8_t*>(p.in_ptr[q])[s];
+      }
+      v |= x << (8 * IB * q);
     }
-    v |= x << (8 * IB * q);
+    return static_cast<InRec>(v);
   }
-  return static_cast<InRec>(v);
 }
 
-// The fused tick: [frozen check] [input ingestion] LOAD, then for each step
-// [SAVE (+checksum, +first-seen record/compare)] ADVANCE, [display checksum],
-// [live store], [mismatch -> freeze].
-template <class G>
+__host__ __device__ inline U128 to_u128(uint16_t c) { return U128{c, 0}; }
+__host__ __device__ inline U128 to_u128(uint64_t c) { return U128{c, 0}; }
+__host__ __device__ inline U128 to_u128(U128 c) { return c; }
+
+// snapshot slot of step k: (f0 + k) % W with f0 % W precomputed (k < 2W)
+__device__ __forceinline__ unsigned step_slot(const KParams& p, int k) {
+  int sl = p.slot0 + k;
+  sl = sl >= p.W ? sl - p.W : sl;
+  sl = sl >= p.W ? sl - p.W : sl;
+  return static_cast<unsigned>(sl);
+}
+
+// The fused tick.  Phase 1 issues every load of the tick (frozen mask, new
+// inputs, the loaded snapshot, the inputs of every step, the first-seen
+// checksums) before any store: on CDNA vmcnt counts loads and stores in issue
+// order, so a load issued after a store would make its consumer wait for the
+// store too.  Phase 2 performs the input-queue writes, phase 3 runs the
+// request stream: per step [SAVE: checksum + snapshot store + first-seen
+// record/compare] ADVANCE, with the state in VGPRs throughout.
+template <class G, bool kPacked>
 __global__ void __launch_bounds__(256) tick_kernel(const KParams p) {
   using InRec = typename G::InRec;
   using CS = typename G::CS;
   constexpr int NW = G::NW;
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= p.Spad) return;
+  const unsigned s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= static_cast<unsigned>(p.S)) return;
   {
-    const int wave0 = __builtin_amdgcn_readfirstlane(s) & ~63;
+    const unsigned wave0 = __builtin_amdgcn_readfirstlane(s) & ~63u;
     const unsigned long long fw = p.frozen[wave0 >> 6];
     if ((fw >> (s & 63)) & 1ull) return;  // advance_frame keeps returning Err for this session
   }
-  if (s >= p.S) return;
-  const int Spad = p.Spad;
+  const unsigned Spad = static_cast<unsigned>(p.Spad);
   InRec* __restrict__ ring = reinterpret_cast<InRec*>(p.ring);
   CS* __restrict__ csa = reinterpret_cast<CS*>(p.cs);
-  CS* __restrict__ fsa = reinterpret_cast<CS*>(p.fs);
+  const CS* __restrict__ fsa = reinterpret_cast<const CS*>(p.fs);
+  const unsigned slot_words = static_cast<unsigned>(NW) * Spad;
 
-  // InputQueue::add_input for every handle (input_queue.rs:149-239): the
-  // delay-fill replication, then the new inputs at frame current + delay.
-  if (p.n_repl > 0) {
-    const InRec v = ring[static_cast<size_t>(p.repl_src) * Spad + s];
-    for (int r = 0; r < p.n_repl; ++r) ring[static_cast<size_t>(p.repl_dst[r]) * Spad + s] = v;
-  }
-  if (p.in_mode != 0 && p.user_slot >= 0) ring[static_cast<size_t>(p.user_slot) * Spad + s] = gather_new_input<G>(p, s);
-
+  // ---- phase 1: loads
+  const bool has_new = p.in_mode != 0 && p.user_slot >= 0;
+  const InRec newin = gather_new_input<G, kPacked>(p, s);
+  const InRec replv = ring[static_cast<unsigned>(p.repl_src) * Spad + s];
   uint32_t w[NW];
   if (p.load_slot >= 0)
-    load_words<NW>(p.snap + static_cast<size_t>(p.load_slot) * NW * Spad, Spad, s, w);
+    load_words<NW>(p.snap + static_cast<unsigned>(p.load_slot) * slot_words, static_cast<int>(Spad), static_cast<int>(s), w);
   else
-    load_words<NW>(p.live, Spad, s, w);
+    load_words<NW>(p.live, static_cast<int>(Spad), static_cast<int>(s), w);
 
-  CsCtx ctx{p.seed, static_cast<uint32_t>(s), p.nonce_base};
+  InRec in[kChunk];
+  CS fsv[kChunk];
+  auto prefetch = [&](int base) {
+#pragma unroll
+    for (int k = 0; k < kChunk; ++k) {
+      const int kk = base + k < p.n_steps ? base + k : base;  // clamp: always a valid address
+      in[k] = ring[static_cast<unsigned>((p.f0 + kk) & (kQueueLen - 1)) * Spad + s];
+      fsv[k] = fsa[step_slot(p, kk) * Spad + s];
+    }
+  };
+  prefetch(0);
+
+  // ---- phase 2: InputQueue::add_input for every handle (input_queue.rs:149-239):
+  // delay-fill replication, then the new inputs at frame current + delay.
+  for (int r = 0; r < p.n_repl; ++r) ring[static_cast<unsigned>(p.repl_dst[r]) * Spad + s] = replv;
+  if (has_new) ring[static_cast<unsigned>(p.user_slot) * Spad + s] = newin;
+  auto patch = [&](int base) {  // prefetched slots that phase 2 just wrote
+#pragma unroll
+    for (int k = 0; k < kChunk; ++k) {
+      const int slot = (p.f0 + base + k) & (kQueueLen - 1);
+      for (int r = 0; r < p.n_repl; ++r)
+        if (slot == p.repl_dst[r]) in[k] = replv;
+      if (has_new && slot == p.user_slot) in[k] = newin;
+    }
+  };
+  patch(0);
+
+  // ---- phase 3: the request stream
+  CsCtx ctx{p.seed, s, p.nonce_base};
   int32_t mismatch = kNullFrame;
   for (int base = 0; base < p.n_steps; base += kChunk) {
-    InRec in[kChunk];
-#pragma unroll
-    for (int k = 0; k < kChunk; ++k)
-      if (base + k < p.n_steps) in[k] = ring[static_cast<size_t>((p.f0 + base + k) & (kQueueLen - 1)) * Spad + s];
+    if (base > 0) {
+      prefetch(base);
+      patch(base);
+    }
 #pragma unroll
     for (int k = 0; k < kChunk; ++k) {
       const int step = base + k;
@@ -180,13 +228,13 @@ __global__ void __launch_bounds__(256) tick_kernel(const KParams p) {
       if (mode != SAVE_NONE) {  // SaveGameState{cell, f}: checksum, cell.save
         ctx.nonce = p.nonce_base + static_cast<uint32_t>(step);
         const CS c = G::checksum(w, f, ctx);
-        const size_t slot = static_cast<size_t>(f % p.W);
-        store_words<NW>(p.snap + slot * NW * Spad, Spad, s, w);
+        const unsigned slot = step_slot(p, step);
+        store_words<NW>(p.snap + slot * slot_words, static_cast<int>(Spad), static_cast<int>(s), w);
         csa[slot * Spad + s] = c;
         if (mode == SAVE_RECORD) {
-          fsa[slot * Spad + s] = c;
+          reinterpret_cast<CS*>(p.fs)[slot * Spad + s] = c;
         } else if (mode == SAVE_COMPARE) {
-          if (c != fsa[slot * Spad + s]) mismatch = f;  // newest mismatching frame wins
+          if (c != fsv[k]) mismatch = f;  // newest mismatching frame wins
         }
       }
       G::advance(w, in[k], p.disc_mask, &p.counters[1]);  // AdvanceFrame{inputs}
@@ -200,17 +248,14 @@ __global__ void __launch_bounds__(256) tick_kernel(const KParams p) {
     ctx.nonce = p.nonce_base + 255u;
     reinterpret_cast<CS*>(p.last_cs)[s] = G::checksum(w, p.f0 + p.n_steps, ctx);
   }
-  if (p.live_out || mismatch != kNullFrame) store_words<NW>(p.live, Spad, s, w);
+  if (p.live_out || mismatch != kNullFrame) store_words<NW>(p.live, static_cast<int>(Spad), static_cast<int>(s), w);
   if (mismatch != kNullFrame) {
     p.err[s] = mismatch;
+    p.live_frame[s] = p.f0 + p.n_steps;  // the session stops at the end of this tick
     atomicOr(&p.frozen[s >> 6], 1ull << (s & 63));
     atomicAdd(&p.counters[0], 1u);
   }
 }
-
-__host__ __device__ inline U128 to_u128(uint16_t c) { return U128{c, 0}; }
-__host__ __device__ inline U128 to_u128(uint64_t c) { return U128{c, 0}; }
-__host__ __device__ inline U128 to_u128(U128 c) { return c; }
 
 template <class G>
 __global__ void report_kernel(const typename G::CS* __restrict__ cs, const int32_t* __restrict__ err, int S,
@@ -271,7 +316,10 @@ struct GameOpsT final : GameOps {
   }
   hipError_t launch_tick(const KParams& p, int block, hipStream_t st) const override {
     const int grid = (p.Spad + block - 1) / block;
-    hipLaunchKernelGGL(tick_kernel<G>, dim3(grid), dim3(block), 0, st, p);
+    if (p.in_mode == 2)
+      hipLaunchKernelGGL((tick_kernel<G, true>), dim3(grid), dim3(block), 0, st, p);
+    else
+      hipLaunchKernelGGL((tick_kernel<G, false>), dim3(grid), dim3(block), 0, st, p);
     return hipGetLastError();
   }
   hipError_t launch_report(const void* cs, const int32_t* err, int S, int32_t frame, void* out,
@@ -322,6 +370,7 @@ struct rb_batch {
   void* last_cs = nullptr;
   void* periodic_cs = nullptr;
   int32_t* err = nullptr;
+  int32_t* live_frame = nullptr;
   unsigned long long* frozen = nullptr;
   uint32_t* counters = nullptr;
   // input staging for host pointers: [2][P][S*input_bytes]
@@ -363,8 +412,8 @@ rb_status destroy_device(rb_batch* b) {
   if (b->plan_only) return RB_OK;
   (void)hipSetDevice(b->device);
   if (b->stream) (void)hipStreamSynchronize(b->stream);
-  void* ptrs[] = {b->snap, b->live, b->cs, b->fs, b->ring, b->last_cs, b->periodic_cs, b->err, b->frozen,
-                  b->counters, b->stage_dev};
+  void* ptrs[] = {b->snap, b->live, b->cs, b->fs, b->ring, b->last_cs, b->periodic_cs, b->err, b->live_frame,
+                  b->frozen, b->counters, b->stage_dev};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   if (b->stage_host) (void)hipHostFree(b->stage_host);
@@ -390,19 +439,23 @@ rb_status launch_program(rb_batch* b, const TickProgram& tp, bool ingest, bool d
   p.last_cs = b->last_cs;
   p.periodic_cs = b->periodic_cs;
   p.err = b->err;
+  p.live_frame = b->live_frame;
   p.frozen = b->frozen;
   p.counters = b->counters;
   p.S = b->S;
   p.Spad = b->Spad;
   p.W = b->W;
+  for (int i = 0; i < 4; ++i) p.in_ptr[i] = b->ring;  // valid dummies: the kernel always loads
+  p.repl_src = 0;
   if (ingest) {
     p.in_mode = b->in_mode;
-    for (int i = 0; i < 4; ++i) p.in_ptr[i] = b->in_ptr[i];
+    for (int i = 0; i < 4; ++i)
+      if (b->in_ptr[i]) p.in_ptr[i] = b->in_ptr[i];
     p.user_slot = tp.user_slot;
     p.n_repl = static_cast<int32_t>(tp.repl_dst.size());
     if (p.n_repl > kMaxRepl) return fail(b, RB_INVALID_REQUEST, "input delay above 8 is not supported by the device batch");
     for (int i = 0; i < p.n_repl; ++i) p.repl_dst[i] = tp.repl_dst[i];
-    p.repl_src = tp.repl_src;
+    if (p.n_repl > 0) p.repl_src = tp.repl_src;
   } else {
     p.in_mode = 0;
     p.user_slot = -1;
@@ -410,7 +463,11 @@ rb_status launch_program(rb_batch* b, const TickProgram& tp, bool ingest, bool d
   p.load_slot = tp.load ? tp.load_frame % b->W : -1;
   p.f0 = tp.f0;
   p.n_steps = tp.n_steps;
-  for (int k = 0; k < tp.n_steps; ++k) p.save_modes[k >> 4] |= static_cast<uint32_t>(tp.save_mode[k] & 3u) << ((k & 15) * 2);
+  p.slot0 = tp.f0 % b->W;
+  if (tp.n_steps > 2 * b->W) return fail(b, RB_PANIC, "tick program longer than two snapshot rings");
+  for (int k = 0; k < tp.n_steps; ++k) {
+    p.save_modes[k >> 4] |= static_cast<uint32_t>(tp.save_mode[k] & 3u) << ((k & 15) * 2);
+  }
   p.live_out = tp.live_out ? 1 : 0;
   p.periodic_step = periodic_step;
   p.display = display ? 1 : 0;
@@ -474,6 +531,8 @@ rb_status rb_synctest_create(const rb_config* cfg, rb_batch** out) {
     return fail(nullptr, RB_INVALID_REQUEST, "negative or zero size in rb_config");
   // builder.rs:342-347
   if (cfg->check_distance >= cfg->max_prediction) return fail(nullptr, RB_INVALID_REQUEST, "Check distance too big.");
+  if (static_cast<uint64_t>(cfg->max_prediction) * 64 * ((static_cast<uint64_t>(cfg->num_sessions) + 63) / 64 * 64) >= (1ull << 32))
+    return fail(nullptr, RB_INVALID_REQUEST, "batch too large for 32-bit snapshot offsets");
   if (cfg->max_prediction > kMaxSteps)
     return fail(nullptr, RB_INVALID_REQUEST, "max_prediction above 64 is not supported by the device batch");
   if (cfg->input_delay > kQueueLen - cfg->max_prediction - 2)
@@ -520,6 +579,7 @@ rb_status rb_synctest_create(const rb_config* cfg, rb_batch** out) {
   HIP_CREATE(hipMalloc(&b->last_cs, Sp * b->ops->cs_bytes));
   HIP_CREATE(hipMalloc(&b->periodic_cs, Sp * b->ops->cs_bytes));
   HIP_CREATE(hipMalloc(&b->err, Sp * 4));
+  HIP_CREATE(hipMalloc(&b->live_frame, Sp * 4));
   HIP_CREATE(hipMalloc(&b->frozen, Sp / 64 * 8));
   HIP_CREATE(hipMalloc(&b->counters, 16));
   const size_t stage = 2ull * b->P * Sp * b->ops->input_bytes;
@@ -536,6 +596,7 @@ rb_status rb_synctest_create(const rb_config* cfg, rb_batch** out) {
   HIP_CREATE(hipMemsetAsync(b->last_cs, 0, Sp * b->ops->cs_bytes, b->stream));
   HIP_CREATE(hipMemsetAsync(b->periodic_cs, 0, Sp * b->ops->cs_bytes, b->stream));
   HIP_CREATE(hipMemsetAsync(b->err, 0xff, Sp * 4, b->stream));  // NULL_FRAME
+  HIP_CREATE(hipMemsetAsync(b->live_frame, 0xff, Sp * 4, b->stream));
   HIP_CREATE(hipMemsetAsync(b->frozen, 0, Sp / 64 * 8, b->stream));
   HIP_CREATE(hipMemsetAsync(b->counters, 0, 16, b->stream));
   // State::new for every session (ex_game.rs:234-257), host-evaluated once.
@@ -655,6 +716,22 @@ rb_status rb_advance_frame(rb_batch* b) {
   return result;
 }
 
+rb_status rb_run_ticks(rb_batch* b, int32_t n_ticks, const void* inputs, int64_t tick_stride_bytes,
+                       int32_t on_device, int32_t* ticks_done) {
+  const uint8_t* base = static_cast<const uint8_t*>(inputs);
+  const size_t player_bytes = static_cast<size_t>(b->S) * b->ops->input_bytes;
+  int32_t done = 0;
+  rb_status st = RB_OK;
+  for (; done < n_ticks; ++done) {
+    const uint8_t* t = base + static_cast<int64_t>(done) * tick_stride_bytes;
+    for (int h = 0; h < b->P && st == RB_OK; ++h) st = rb_add_local_input(b, h, t + h * player_bytes, on_device);
+    if (st == RB_OK) st = rb_advance_frame(b);
+    if (st != RB_OK) break;
+  }
+  if (ticks_done) *ticks_done = done;
+  return st;
+}
+
 rb_status rb_synchronize(rb_batch* b) {
   if (b->plan_only) return RB_OK;
   HIP_TRY(b, hipStreamSynchronize(b->stream));
@@ -736,13 +813,15 @@ rb_status rb_read_live(rb_batch* b, void* images, uint64_t* display_checksums, i
   if (st != RB_OK) return st;
   std::vector<uint8_t> dcs(static_cast<size_t>(b->Spad) * b->ops->cs_bytes);
   HIP_TRY(b, hipMemcpy(dcs.data(), b->last_cs, dcs.size(), hipMemcpyDeviceToHost));
-  std::vector<int32_t> e(b->Spad);
+  std::vector<int32_t> e(b->Spad), lf(b->Spad);
   HIP_TRY(b, hipMemcpy(e.data(), b->err, b->Spad * 4, hipMemcpyDeviceToHost));
+  HIP_TRY(b, hipMemcpy(lf.data(), b->live_frame, b->Spad * 4, hipMemcpyDeviceToHost));
   std::vector<uint32_t> w(b->ops->nw);
   for (int s = 0; s < b->S; ++s) {
     words_of(b, planes, s, w.data());
     // a failed session stopped advancing at the end of the tick that detected it
-    if (images) b->ops->image(w.data(), cur, static_cast<uint8_t*>(images) + static_cast<size_t>(s) * b->ops->image_bytes);
+    const int32_t fr = e[s] != kNullFrame ? lf[s] : cur;
+    if (images) b->ops->image(w.data(), fr, static_cast<uint8_t*>(images) + static_cast<size_t>(s) * b->ops->image_bytes);
     if (display_checksums) display_checksums[s] = b->ops->display ? b->ops->cs_at(dcs.data(), s).lo : 0;
   }
   if (display_frame) *display_frame = b->ops->display ? b->display_frame : kNullFrame;

@@ -114,6 +114,35 @@ def _raise(lib, handle, status: int):
     raise Panic(msg or f"rb_status {status}")
 
 
+class RequestList:
+    """The Vec<GGRSRequest> of one advance_frame, decoded on first access."""
+
+    __slots__ = ("_k", "_f", "_n", "_items")
+
+    def __init__(self, kinds, frames, n):
+        self._k, self._f, self._n, self._items = kinds, frames, n, None
+
+    def _decode(self):
+        if self._items is None:
+            self._items = [GGRSRequest(RequestKind(self._k[i]), self._f[i]) for i in range(self._n)]
+        return self._items
+
+    def __len__(self):
+        return self._n
+
+    def __iter__(self):
+        return iter(self._decode())
+
+    def __getitem__(self, i):
+        return self._decode()[i]
+
+    def __eq__(self, other):
+        return list(self._decode()) == list(other)
+
+    def __repr__(self):
+        return repr(self._decode())
+
+
 # --------------------------------------------------------------------------- builder (builder.rs)
 class SessionBuilder:
     """builder.rs:32-377, SyncTest subset, plus the batch size and device."""
@@ -249,9 +278,10 @@ class SyncTestSession:
         self._keep.append(keep)
         _raise(self._lib, self._h, self._lib.rb_add_local_inputs_packed(self._h, ptr, dev))
 
-    def advance_frame(self) -> List[GGRSRequest]:  # :85-146
+    def advance_frame(self) -> "RequestList":  # :85-146
         """Runs SyncTestSession::advance_frame and the game's handle_requests
-        for every session; returns the request stream that was executed."""
+        for every session; returns the request stream that was executed
+        (a list of GGRSRequest, decoded lazily)."""
         st = self._lib.rb_advance_frame(self._h)
         self._keep.clear()
         if st == L.RB_MISMATCHED_CHECKSUM:
@@ -259,13 +289,28 @@ class SyncTestSession:
         _raise(self._lib, self._h, st)
         return self.last_requests()
 
+    def run_ticks(self, inputs) -> int:
+        """``len(inputs)`` x (add_local_input for every handle + advance_frame)
+        in one native call; ``inputs`` is [T, num_players, num_sessions]
+        (numpy, or a CUDA tensor kept on the device)."""
+        T = int(inputs.shape[0])
+        per_tick = self._num_players * self.num_sessions
+        ptr, dev, keep = self._as_input(inputs, T * per_tick) if T else (None, 0, None)
+        done = ctypes.c_int32()
+        st = self._lib.rb_run_ticks(self._h, T, ptr, per_tick * np.dtype(self.input_dtype).itemsize, dev,
+                                    ctypes.byref(done))
+        if st == L.RB_MISMATCHED_CHECKSUM:
+            raise MismatchedChecksum(self.mismatches())
+        _raise(self._lib, self._h, st)
+        return done.value
+
     # -- batch extras
-    def last_requests(self) -> List[GGRSRequest]:
+    def last_requests(self) -> "RequestList":
         cap = 4 * self._max_prediction + 8
         k = (ctypes.c_int32 * cap)()
         f = (ctypes.c_int32 * cap)()
         n = self._lib.rb_last_requests(self._h, k, f, cap)
-        return [GGRSRequest(RequestKind(k[i]), f[i]) for i in range(n)]
+        return RequestList(k, f, n)
 
     def mismatches(self) -> np.ndarray:
         out = np.empty(self.num_sessions, dtype=np.int32)

@@ -120,6 +120,14 @@ rb_status rb_add_local_inputs_packed(rb_batch* b, const void* inputs, int32_t on
  * asynchronous and mismatches are read with rb_mismatches. */
 rb_status rb_advance_frame(rb_batch* b);
 
+/* n_ticks x (add_local_input for every handle + advance_frame) in one call:
+ * tick t reads its inputs at inputs + t*tick_stride_bytes, laid out
+ * [num_players][num_sessions] Input values (host or device memory).  Stops at
+ * the first non-RB_OK status (returned); *ticks_done = completed ticks.  The
+ * host-side loop of a replay/batch job without per-tick FFI overhead. */
+rb_status rb_run_ticks(rb_batch* b, int32_t n_ticks, const void* inputs, int64_t tick_stride_bytes,
+                       int32_t on_device, int32_t* ticks_done);
+
 /* SyncLayer::current_frame of the batch (sync_layer.rs:110-112). */
 int32_t rb_current_frame(const rb_batch* b);
 int32_t rb_num_sessions(const rb_batch* b);
