@@ -204,7 +204,7 @@ def main():
                 "traffic": traffic,
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "kernel_avg_us": avg_kernel_s * 1e6,
-                "kernel": "tick_kernel<ExGame<2>>",
+                "kernel": f"steady_kernel<ExGame<{P},true>,{cd}> (fused steady-state ticks)",
             },
             "cpu_baseline": None,
         }

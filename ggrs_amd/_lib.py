@@ -32,6 +32,7 @@ RB_GAME_STUB_ENUM = 3
 RB_GAME_STUB_RANDOM_CS = 4
 
 RB_FLAG_CHECKED = 1
+RB_FLAG_LANE_PER_SESSION = 2
 
 
 class RbConfig(ctypes.Structure):

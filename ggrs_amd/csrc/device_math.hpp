@@ -56,56 +56,49 @@ __device__ __forceinline__ double cos_poly(double x2) {
   return __builtin_fma(x6, cp2, c);
 }
 
-__device__ __forceinline__ SinCos sincosf_glibc(float y, uint32_t* unexpected) {
-  const float pio4 = 0x1.921FB6p-1f;
-  double x = y;
-  SinCos r;
-  if (abstop12(y) < abstop12(pio4)) {
-    if (abstop12(y) < abstop12(0x1p-12f)) {
-      r.s = y;
-      r.c = 1.0f;
-      return r;
-    }
-    double x2 = x * x;
-    r.s = static_cast<float>(sin_poly(x, x2));
-    r.c = static_cast<float>(cos_poly(x2));
-    return r;
-  }
-  if (abstop12(y) < abstop12(120.0f)) {
-    // reduce_fast, !TOINT_INTRINSICS form (x86_64): hpi_inv prescaled by 2^24.
-    const double hpi_inv = 0x1.45F306DC9C883p+23, hpi = 0x1.921FB54442D18p0;
-    double rr = x * hpi_inv;
-    int n = (static_cast<int32_t>(rr) + 0x800000) >> 24;
-    double xr = __builtin_fma(-static_cast<double>(n), hpi, x);
-    double sgn = ((n & 3) == 1 || (n & 3) == 2) ? -1.0 : 1.0;  // sign[4] = {1,-1,-1,1}
-    double xs = xr * sgn;
-    double x2 = xr * xr;
-    double sp = sin_poly(xs, x2);
-    double cp = cos_poly(x2);
-    if (n & 2) cp = -cp;  // __sincosf_table[1]
-    // sinf: n even -> sine poly, odd -> cosine poly; cosf uses n ^ 1.
-    r.s = static_cast<float>((n & 1) ? cp : sp);
-    r.c = static_cast<float>((n & 1) ? sp : cp);
-    return r;
-  }
+// |y| >= 120: not restated (ex_game never gets there); the library routines,
+// out of line so they do not bloat the hot path, and counted.
+__device__ __noinline__ SinCos sincosf_large(float y, uint32_t* unexpected) {
   if (unexpected) atomicAdd(unexpected, 1u);
+  SinCos r;
   r.s = sinf(y);
   r.c = cosf(y);
   return r;
 }
 
-// f32::rem_euclid (r = x % rhs; r < 0 ? r + |rhs| : r).  fmod is exact; for
-// |x| < 2|rhs| it is x or x -/+ rhs (Sterbenz), else the library fmodf.
-__device__ __forceinline__ float rem_euclid(float x, float rhs) {
-  float ay = __builtin_fabsf(rhs), ax = __builtin_fabsf(x);
-  float r;
-  if (ax < ay) {
-    r = x;
-  } else if (ax < 2.0f * ay) {
-    r = __builtin_copysignf(ax - ay, x);
-  } else {
-    r = fmodf(x, rhs);
+__device__ __forceinline__ SinCos sincosf_glibc(float y, uint32_t* unexpected) {
+  // |y| < pi/4 takes glibc's unreduced branch: reduce_fast yields n = 0 and
+  // xr = y exactly there, so one straight-line path serves both; |y| < 2^-12
+  // returns (y, 1) as glibc does.
+  const double hpi_inv = 0x1.45F306DC9C883p+23, hpi = 0x1.921FB54442D18p0;  // !TOINT_INTRINSICS form (x86_64)
+  const double x = y;
+  const int n = (static_cast<int32_t>(x * hpi_inv) + 0x800000) >> 24;
+  const double xr = __builtin_fma(-static_cast<double>(n), hpi, x);
+  const double xs = ((n & 3) == 1 || (n & 3) == 2) ? -xr : xr;  // sign[4] = {1,-1,-1,1}
+  const double x2 = xr * xr;
+  const float sp = static_cast<float>(sin_poly(xs, x2));
+  const double cpd = cos_poly(x2);
+  const float cp = static_cast<float>((n & 2) ? -cpd : cpd);  // __sincosf_table[1]
+  SinCos r;
+  // sinf: n even -> sine poly, odd -> cosine poly; cosf uses n ^ 1.
+  r.s = (n & 1) ? cp : sp;
+  r.c = (n & 1) ? sp : cp;
+  const uint32_t top = abstop12(y);
+  if (top < abstop12(0x1p-12f)) {
+    r.s = y;
+    r.c = 1.0f;
   }
+  if (__builtin_expect(top >= abstop12(120.0f), 0)) r = sincosf_large(y, unexpected);
+  return r;
+}
+
+// f32::rem_euclid (r = x % rhs; r < 0 ? r + |rhs| : r).  fmod is exact; for
+// |x| < 2|rhs| it is x or x -/+ rhs (Sterbenz), else the library fmodf (out of line).
+__device__ __noinline__ float fmodf_slow(float x, float y) { return fmodf(x, y); }
+__device__ __forceinline__ float rem_euclid(float x, float rhs) {
+  const float ay = __builtin_fabsf(rhs), ax = __builtin_fabsf(x);
+  float r = ax < ay ? x : __builtin_copysignf(ax - ay, x);
+  if (__builtin_expect(!(ax < 2.0f * ay), 0)) r = fmodf_slow(x, rhs);
   return r < 0.0f ? r + ay : r;
 }
 

@@ -2,13 +2,17 @@
 //
 // A game plugs into the engine with (the `Config` trait of lib.rs:240-262 plus
 // the user's handle_requests of ex_game.rs:76-84, as device code):
-//   NW        state words per session stored in a snapshot slot (u32 each)
+//   kLanes    lanes per session (1, 2 or 4): a session's state may be sliced
+//             over a lane group that advances in lock-step; the checksum is
+//             then combined across the group with DPP lane swaps
+//   NWL       state words per lane stored in a snapshot slot (u32 each)
 //   InRec     one session's packed inputs for one frame (P Input values)
 //   CS        checksum type stored per cell (zero-extended to u128 on export)
-//   init      host: State::new words
-//   advance   device: one AdvanceFrame on the register-resident state
-//   checksum  device: the checksum the game's save_game_state stores
-//   image     host: canonical byte image of (frame, words) for read-back
+//   init      host: State::new, words [kLanes][NWL]
+//   advance   device: one AdvanceFrame on the lane's register-resident slice
+//   checksum  device: the checksum the game's save_game_state stores (the
+//             whole session's value, in every lane of the group)
+//   image     host: canonical byte image of (frame, words [kLanes][NWL])
 // The cell's frame tag is stored once per slot (batch-uniform): every game
 // here asserts state.frame == cell frame on save (ex_game.rs:89,
 // stubs.rs:53,93, stubs_enum.rs:185), so the per-session frame word is
@@ -49,16 +53,28 @@ struct InRecOf<2> {
   using T = uint16_t;
 };
 
+// Sum of a u32 over the lane group of a session (groups of 1, 2 or 4
+// consecutive lanes): DPP quad_perm swaps, no LDS round trip.
+template <int L>
+__device__ __forceinline__ uint32_t group_sum(uint32_t v) {
+  if constexpr (L >= 2) v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0xB1, 0xF, 0xF, false));  // [1,0,3,2]
+  if constexpr (L >= 4) v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x4E, 0xF, 0xF, false));  // [2,3,0,1]
+  return v;
+}
+
 // ============================================================================
-// examples/ex_game/ex_game.rs
+// examples/ex_game/ex_game.rs — one lane per player (kSplit) or per session
 // ============================================================================
-template <int P>
+template <int P, bool kSplit>
 struct ExGame {
   static_assert(P >= 1 && P <= 4, "ex_game supports 1..4 players (ex_game.rs:65)");
   static constexpr int kPlayers = P;
-  static constexpr int NW = 5 * P;  // bincode order: positions (x,y)*P, velocities (x,y)*P, rotations*P
+  static constexpr int kLanes = kSplit ? (P == 1 ? 1 : (P == 2 ? 2 : 4)) : 1;
+  static constexpr int kPlayersPerLane = kSplit ? 1 : P;
+  static constexpr int NWL = 5 * kPlayersPerLane;  // per player: x, y, vx, vy, rot
   static constexpr int kInputBytes = 1;
   static constexpr int kImageBytes = 36 + 20 * P;  // bincode 1.3 image of State (ex_game.rs:224-231)
+  static constexpr bool kDisplay = true;           // Game::last_checksum / periodic_checksum
   using InRec = typename InRecOf<P>::T;
   using CS = uint16_t;
 
@@ -70,9 +86,15 @@ struct ExGame {
   static constexpr float kWidth = 600.0f, kHeight = 800.0f;
   static constexpr float kPi = 3.14159265358979323846f;
 
+  // byte offsets of player i's fields in the bincode image
+  __host__ __device__ static constexpr int off_x(int i) { return 20 + 8 * i; }
+  __host__ __device__ static constexpr int off_vx(int i) { return 28 + 8 * P + 8 * i; }
+  __host__ __device__ static constexpr int off_rot(int i) { return 36 + 16 * P + 4 * i; }
+
   // State::new (ex_game.rs:234-257), evaluated with the host libm like the
-  // reference (glibc cosf/sinf/fmodf).
-  static void init(uint32_t* w) {
+  // reference (glibc cosf/sinf/fmodf).  words: [kLanes][NWL].
+  static void init(uint32_t* words) {
+    std::memset(words, 0, sizeof(uint32_t) * kLanes * NWL);
     const float r = kWidth / 4.0f;
     for (int i = 0; i < P; ++i) {
       // volatile: keep the compiler from constant-folding libm calls with its
@@ -82,76 +104,15 @@ struct ExGame {
       float x = kWidth / 2.0f + r * std::cos(rot);
       float y = kHeight / 2.0f + r * std::sin(rot);
       float ro = std::fmod(rot + kPi, 2.0f * kPi);
-      std::memcpy(&w[2 * i], &x, 4);
-      std::memcpy(&w[2 * i + 1], &y, 4);
-      w[2 * P + 2 * i] = 0;
-      w[2 * P + 2 * i + 1] = 0;
-      std::memcpy(&w[4 * P + i], &ro, 4);
+      uint32_t* w = words + (kSplit ? i * NWL : 0);
+      const int j = kSplit ? 0 : i;
+      std::memcpy(&w[5 * j + 0], &x, 4);
+      std::memcpy(&w[5 * j + 1], &y, 4);
+      std::memcpy(&w[5 * j + 4], &ro, 4);
     }
   }
 
-  __device__ static uint32_t player_input(InRec rec, int p) { return (static_cast<uint32_t>(rec) >> (8 * p)) & 0xffu; }
-
-  // State::advance (ex_game.rs:259-321).  Compiled with -ffp-contract=off:
-  // every f32 operation rounds exactly as the reference's.
-  __device__ static void advance(uint32_t (&w)[NW], InRec rec, uint32_t disconnected_mask, uint32_t* unexpected) {
-#pragma unroll
-    for (int i = 0; i < P; ++i) {
-      const uint32_t input = ((disconnected_mask >> i) & 1u) ? 4u : player_input(rec, i);
-      const float old_x = __uint_as_float(w[2 * i]), old_y = __uint_as_float(w[2 * i + 1]);
-      const float old_vx = __uint_as_float(w[2 * P + 2 * i]), old_vy = __uint_as_float(w[2 * P + 2 * i + 1]);
-      float rot = __uint_as_float(w[4 * P + i]);
-      float vx = old_vx * kFriction;
-      float vy = old_vy * kFriction;
-      const bool up = input & 1u, down = input & 2u, left = input & 4u, right = input & 8u;
-      if (up != down) {  // thrust (:281-284) or brake (:286-289): exactly one of them
-        SinCos sc = sincosf_glibc(rot, unexpected);
-        const float tx = kMovementSpeed * sc.c, ty = kMovementSpeed * sc.s;
-        if (up) {
-          vx = vx + tx;
-          vy = vy + ty;
-        } else {
-          vx = vx - tx;
-          vy = vy - ty;
-        }
-      }
-      if (left != right) rot = rem_euclid(left ? rot - kRotationSpeed : rot + kRotationSpeed, 2.0f * kPi);
-      const float mag = __builtin_sqrtf(vx * vx + vy * vy);
-      if (mag > kMaxSpeed) {
-        vx = (vx * kMaxSpeed) / mag;
-        vy = (vy * kMaxSpeed) / mag;
-      }
-      float x = old_x + vx, y = old_y + vy;
-      x = fminf(fmaxf(x, 0.0f), kWidth);
-      y = fminf(fmaxf(y, 0.0f), kHeight);
-      w[2 * i] = __float_as_uint(x);
-      w[2 * i + 1] = __float_as_uint(y);
-      w[2 * P + 2 * i] = __float_as_uint(vx);
-      w[2 * P + 2 * i + 1] = __float_as_uint(vy);
-      w[4 * P + i] = __float_as_uint(rot);
-    }
-  }
-
-  // Byte offset of state word k inside the bincode image.
-  __host__ __device__ static constexpr int word_offset(int k) {
-    return 20 + 4 * k + (k >= 2 * P ? 8 : 0) + (k >= 4 * P ? 8 : 0);
-  }
-
-  // fletcher16(bincode::serialize(&state)) (ex_game.rs:90-91) from registers.
-  __device__ static CS checksum(const uint32_t (&w)[NW], int32_t frame, const CsCtx&) {
-    constexpr int n = kImageBytes;
-    // constant bytes: num_players and the three Vec lengths (u64 = P, LE) at
-    // offsets 4, 12, 20+8P, 28+16P
-    constexpr uint32_t c1 = 4u * P;
-    constexpr uint32_t c2 = P * static_cast<uint32_t>((n - 4) + (n - 12) + (n - 20 - 8 * P) + (n - 28 - 16 * P));
-    Fl16 a{c1, c2};
-    fl16_word(a, static_cast<uint32_t>(frame), fl16_weights(n, 0));
-#pragma unroll
-    for (int k = 0; k < NW; ++k) fl16_word(a, w[k], fl16_weights(n, word_offset(k)));
-    return fl16_finish(a);
-  }
-
-  static void image(const uint32_t* w, int32_t frame, uint8_t* out) {
+  static void image(const uint32_t* words, int32_t frame, uint8_t* out) {
     std::memset(out, 0, kImageBytes);
     std::memcpy(out, &frame, 4);
     const uint64_t np = P;
@@ -159,9 +120,96 @@ struct ExGame {
     std::memcpy(out + 12, &np, 8);
     std::memcpy(out + 20 + 8 * P, &np, 8);
     std::memcpy(out + 28 + 16 * P, &np, 8);
-    for (int k = 0; k < NW; ++k) std::memcpy(out + word_offset(k), &w[k], 4);
+    for (int i = 0; i < P; ++i) {
+      const uint32_t* w = words + (kSplit ? i * NWL : 5 * i);
+      std::memcpy(out + off_x(i), &w[0], 4);
+      std::memcpy(out + off_x(i) + 4, &w[1], 4);
+      std::memcpy(out + off_vx(i), &w[2], 4);
+      std::memcpy(out + off_vx(i) + 4, &w[3], 4);
+      std::memcpy(out + off_rot(i), &w[4], 4);
+    }
   }
   static U128 cs128(CS c) { return U128{c, 0}; }
+  // canonical word k (bincode order: positions, velocities, rotations) -> (lane, word)
+  static void word_loc(int k, int* lane, int* word) {
+    int i, f;
+    if (k < 2 * P) { i = k / 2; f = k % 2; }
+    else if (k < 4 * P) { i = (k - 2 * P) / 2; f = 2 + (k - 2 * P) % 2; }
+    else { i = k - 4 * P; f = 4; }
+    *lane = kSplit ? i : 0;
+    *word = kSplit ? f : 5 * i + f;
+  }
+  static constexpr int kCanonWords = 5 * P;
+
+  __device__ static uint32_t player_input(InRec rec, int i) { return (static_cast<uint32_t>(rec) >> (8 * i)) & 0xffu; }
+
+  // State::advance (ex_game.rs:259-321) for one player.  Compiled with
+  // -ffp-contract=off: every f32 operation rounds exactly as the reference's.
+  __device__ static void advance_player(uint32_t* w, uint32_t input, uint32_t* unexpected) {
+    const float old_x = __uint_as_float(w[0]), old_y = __uint_as_float(w[1]);
+    const float old_vx = __uint_as_float(w[2]), old_vy = __uint_as_float(w[3]);
+    float rot = __uint_as_float(w[4]);
+    float vx = old_vx * kFriction;
+    float vy = old_vy * kFriction;
+    const bool up = input & 1u, down = input & 2u, left = input & 4u, right = input & 8u;
+    if (up != down) {  // thrust (:281-284) or brake (:286-289): exactly one of them
+      const SinCos sc = sincosf_glibc(rot, unexpected);
+      const float tx = kMovementSpeed * sc.c, ty = kMovementSpeed * sc.s;
+      vx = up ? vx + tx : vx - tx;
+      vy = up ? vy + ty : vy - ty;
+    }
+    if (left != right) rot = rem_euclid(left ? rot - kRotationSpeed : rot + kRotationSpeed, 2.0f * kPi);
+    const float mag = __builtin_sqrtf(vx * vx + vy * vy);
+    if (mag > kMaxSpeed) {
+      vx = (vx * kMaxSpeed) / mag;
+      vy = (vy * kMaxSpeed) / mag;
+    }
+    float x = old_x + vx, y = old_y + vy;
+    x = fminf(fmaxf(x, 0.0f), kWidth);
+    y = fminf(fmaxf(y, 0.0f), kHeight);
+    w[0] = __float_as_uint(x);
+    w[1] = __float_as_uint(y);
+    w[2] = __float_as_uint(vx);
+    w[3] = __float_as_uint(vy);
+    w[4] = __float_as_uint(rot);
+  }
+
+  __device__ static void advance(uint32_t (&w)[NWL], InRec rec, int lane, uint32_t disconnected_mask,
+                                 uint32_t* unexpected) {
+#pragma unroll
+    for (int j = 0; j < kPlayersPerLane; ++j) {
+      const int i = kSplit ? lane : j;  // player index
+      const uint32_t input = ((disconnected_mask >> i) & 1u) ? 4u : player_input(rec, i);  // Disconnected => 4 (:268)
+      advance_player(&w[5 * j], input, unexpected);
+    }
+  }
+
+  // fletcher16(bincode::serialize(&state)) (ex_game.rs:90-91) from registers:
+  // closed-form weighted byte sums per lane, summed over the lane group.
+  __device__ static CS checksum(const uint32_t (&w)[NWL], int32_t frame, int lane, const CsCtx&) {
+    constexpr int n = kImageBytes;
+    // constant bytes: num_players and the three Vec lengths (u64 = P, LE) at
+    // offsets 4, 12, 20+8P, 28+16P
+    constexpr uint32_t c1 = 4u * P;
+    constexpr uint32_t c2 = P * static_cast<uint32_t>((n - 4) + (n - 12) + (n - 20 - 8 * P) + (n - 28 - 16 * P));
+    auto wp = [](int o) { return static_cast<uint32_t>(n - o) * 0x01010101u - 0x03020100u; };  // (n-o, n-o-1, n-o-2, n-o-3)
+    const bool lead = lane == 0;
+    Fl16 a{lead ? c1 : 0u, lead ? c2 : 0u};
+    fl16_word(a, lead ? static_cast<uint32_t>(frame) : 0u, fl16_weights(n, 0));
+#pragma unroll
+    for (int j = 0; j < kPlayersPerLane; ++j) {
+      const int i = kSplit ? lane : j;
+      const uint32_t live = (!kSplit || i < P) ? ~0u : 0u;  // padding lanes of a 4-lane group add nothing
+      fl16_word(a, w[5 * j + 0] & live, wp(off_x(i)));
+      fl16_word(a, w[5 * j + 1] & live, wp(off_x(i) + 4));
+      fl16_word(a, w[5 * j + 2] & live, wp(off_vx(i)));
+      fl16_word(a, w[5 * j + 3] & live, wp(off_vx(i) + 4));
+      fl16_word(a, w[5 * j + 4] & live, wp(off_rot(i)));
+    }
+    a.s1 = group_sum<kLanes>(a.s1);
+    a.s2 = group_sum<kLanes>(a.s2);
+    return fl16_finish(a);
+  }
 };
 
 // ============================================================================
@@ -169,56 +217,64 @@ struct ExGame {
 // ============================================================================
 struct StubGame {
   static constexpr int kPlayers = 2;  // StateStub::advance_frame reads inputs[0], inputs[1]
-  static constexpr int NW = 1;        // state (frame comes from the cell tag)
+  static constexpr int kLanes = 1;
+  static constexpr int NWL = 1;  // state (frame comes from the cell tag)
   static constexpr int kInputBytes = 4;
   static constexpr int kImageBytes = 8;
+  static constexpr bool kDisplay = false;
   using InRec = uint64_t;  // two StubInput{inp:u32}
   using CS = uint64_t;     // DefaultHasher::finish() as u128
 
   static void init(uint32_t* w) { w[0] = 0; }
-  __device__ static uint32_t player_input(InRec rec, int p) { return static_cast<uint32_t>(rec >> (32 * p)); }
-  // stubs.rs:115-125
-  __device__ static void advance(uint32_t (&w)[NW], InRec rec, uint32_t, uint32_t*) {
-    const uint32_t p0 = player_input(rec, 0), p1 = player_input(rec, 1);
-    w[0] = ((p0 + p1) % 2u == 0u) ? w[0] + 2u : w[0] - 1u;
-  }
-  // calculate_hash(&StateStub{frame, state}) (stubs.rs:8-12, 54)
-  __device__ static CS checksum(const uint32_t (&w)[NW], int32_t frame, const CsCtx&) {
-    return siphash13_i32x2(frame, static_cast<int32_t>(w[0]));
-  }
   static void image(const uint32_t* w, int32_t frame, uint8_t* out) {
     std::memcpy(out, &frame, 4);
     std::memcpy(out + 4, &w[0], 4);
   }
   static U128 cs128(CS c) { return U128{c, 0}; }
+  static void word_loc(int, int* lane, int* word) { *lane = 0; *word = 0; }
+  static constexpr int kCanonWords = 1;
+  __device__ static uint32_t player_input(InRec rec, int p) { return static_cast<uint32_t>(rec >> (32 * p)); }
+  // stubs.rs:115-125
+  __device__ static void advance(uint32_t (&w)[NWL], InRec rec, int, uint32_t, uint32_t*) {
+    const uint32_t p0 = player_input(rec, 0), p1 = player_input(rec, 1);
+    w[0] = ((p0 + p1) % 2u == 0u) ? w[0] + 2u : w[0] - 1u;
+  }
+  // calculate_hash(&StateStub{frame, state}) (stubs.rs:8-12, 54)
+  __device__ static CS checksum(const uint32_t (&w)[NWL], int32_t frame, int, const CsCtx&) {
+    return siphash13_i32x2(frame, static_cast<int32_t>(w[0]));
+  }
 };
 
 // tests/stubs_enum.rs GameStubEnum: EnumInput #[repr(u8)] {Val1, Val2}
 struct StubEnumGame {
   static constexpr int kPlayers = 2;
-  static constexpr int NW = 1;
+  static constexpr int kLanes = 1;
+  static constexpr int NWL = 1;
   static constexpr int kInputBytes = 1;
   static constexpr int kImageBytes = 8;
+  static constexpr bool kDisplay = false;
   using InRec = uint16_t;
   using CS = uint64_t;
   static void init(uint32_t* w) { w[0] = 0; }
-  __device__ static uint32_t player_input(InRec rec, int p) { return (static_cast<uint32_t>(rec) >> (8 * p)) & 0xffu; }
-  // stubs_enum.rs:206-216
-  __device__ static void advance(uint32_t (&w)[NW], InRec rec, uint32_t, uint32_t*) {
-    w[0] = (player_input(rec, 0) == player_input(rec, 1)) ? w[0] + 2u : w[0] - 1u;
-  }
-  __device__ static CS checksum(const uint32_t (&w)[NW], int32_t frame, const CsCtx&) {
-    return siphash13_i32x2(frame, static_cast<int32_t>(w[0]));
-  }
   static void image(const uint32_t* w, int32_t frame, uint8_t* out) { StubGame::image(w, frame, out); }
   static U128 cs128(CS c) { return U128{c, 0}; }
+  static void word_loc(int, int* lane, int* word) { *lane = 0; *word = 0; }
+  static constexpr int kCanonWords = 1;
+  __device__ static uint32_t player_input(InRec rec, int p) { return (static_cast<uint32_t>(rec) >> (8 * p)) & 0xffu; }
+  // stubs_enum.rs:206-216
+  __device__ static void advance(uint32_t (&w)[NWL], InRec rec, int, uint32_t, uint32_t*) {
+    w[0] = (player_input(rec, 0) == player_input(rec, 1)) ? w[0] + 2u : w[0] - 1u;
+  }
+  __device__ static CS checksum(const uint32_t (&w)[NWL], int32_t frame, int, const CsCtx&) {
+    return siphash13_i32x2(frame, static_cast<int32_t>(w[0]));
+  }
 };
 
 // tests/stubs.rs:67-106 RandomChecksumGameStub: a fresh random u128 on every
 // save (counter-based: splitmix64 of seed/session/save nonce).
 struct StubRandomCsGame : StubGame {
   using CS = U128;
-  __device__ static CS checksum(const uint32_t (&)[NW], int32_t frame, const CsCtx& c) {
+  __device__ static CS checksum(const uint32_t (&)[NWL], int32_t frame, int, const CsCtx& c) {
     const uint64_t k = c.seed ^ (static_cast<uint64_t>(c.session) << 32) ^ c.nonce ^ (static_cast<uint64_t>(frame) << 48);
     return U128{splitmix64(k), splitmix64(k ^ 0x5bd1e995ULL)};
   }

@@ -195,6 +195,19 @@ class SessionBuilder:
         self._cfg.seed = int(seed) & (2**64 - 1)
         return self
 
+    def with_lane_per_session(self, on: bool) -> "SessionBuilder":
+        """ex_game: one lane per session (True) instead of one lane per player."""
+        if on:
+            self._cfg.flags |= L.RB_FLAG_LANE_PER_SESSION
+        else:
+            self._cfg.flags &= ~L.RB_FLAG_LANE_PER_SESSION
+        return self
+
+    def with_debug_flags(self, flags: int) -> "SessionBuilder":
+        """Experiment knobs for kernel attribution (results are WRONG when set)."""
+        self._cfg.reserved[0] = int(flags)
+        return self
+
     def with_block_size(self, block: int) -> "SessionBuilder":
         self._cfg.block_size = int(block)
         return self
@@ -261,7 +274,9 @@ class SyncTestSession:
             if inputs.element_size() != np.dtype(self.input_dtype).itemsize:
                 raise InvalidRequest("device inputs have the wrong element size for this game's Input")
             return ctypes.c_void_p(inputs.data_ptr()), 1, inputs
-        arr = np.ascontiguousarray(np.broadcast_to(np.asarray(inputs), (count,)), dtype=self.input_dtype)
+        a = np.asarray(inputs)
+        a = a.reshape(-1) if a.size == count else np.broadcast_to(a, (count,))
+        arr = np.ascontiguousarray(a, dtype=self.input_dtype)
         return arr.ctypes.data_as(ctypes.c_void_p), 0, arr
 
     def add_local_input(self, player_handle: int, inputs) -> None:  # :61-74
@@ -337,14 +352,14 @@ class SyncTestSession:
         return img, cs
 
     def read_live(self):
-        """(images [S, state_bytes], display checksums [S] u64, display frame)."""
+        """(images [S, state_bytes], display checksums [S] u64, display frames [S] i32)."""
         img = np.empty((self.num_sessions, self.state_bytes), dtype=np.uint8)
         dcs = np.empty(self.num_sessions, dtype=np.uint64)
-        fr = ctypes.c_int32()
+        fr = np.empty(self.num_sessions, dtype=np.int32)
         _raise(self._lib, self._h, self._lib.rb_read_live(
             self._h, img.ctypes.data_as(ctypes.c_void_p),
-            dcs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), ctypes.byref(fr)))
-        return img, dcs, fr.value
+            dcs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), fr.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
+        return img, dcs, fr
 
     def export_checksum_report(self, frame: int, dev_ptr: int) -> None:
         """Write [S] rb_checksum_report (32 B each) for ``frame`` to device memory."""

@@ -53,7 +53,8 @@ typedef enum rb_game {
 /* GGRSRequest kinds (lib.rs:170-194) for rb_last_requests. */
 typedef enum rb_request_kind { RB_REQ_SAVE = 0, RB_REQ_LOAD = 1, RB_REQ_ADVANCE = 2 } rb_request_kind;
 
-#define RB_FLAG_CHECKED 1u /* advance_frame reports MismatchedChecksum synchronously, like the reference (default) */
+#define RB_FLAG_CHECKED 1u          /* advance_frame reports MismatchedChecksum synchronously, like the reference (default) */
+#define RB_FLAG_LANE_PER_SESSION 2u /* ex_game: one lane per session instead of one lane per player (tuning/A-B only) */
 
 /* SessionBuilder fields used by start_synctest_session (builder.rs:32-52). */
 typedef struct rb_config {
@@ -122,9 +123,14 @@ rb_status rb_advance_frame(rb_batch* b);
 
 /* n_ticks x (add_local_input for every handle + advance_frame) in one call:
  * tick t reads its inputs at inputs + t*tick_stride_bytes, laid out
- * [num_players][num_sessions] Input values (host or device memory).  Stops at
- * the first non-RB_OK status (returned); *ticks_done = completed ticks.  The
- * host-side loop of a replay/batch job without per-tick FFI overhead. */
+ * [num_players][num_sessions] Input values (host or device memory).  The host
+ * bookkeeping runs tick by tick as in rb_advance_frame; consecutive
+ * steady-state ticks (current frame > check_distance, 1 <= check_distance <= 8)
+ * execute as ONE fused device launch.  A session whose resimulation
+ * mismatches stops advancing (as with per-tick calls) while the others run
+ * on; with RB_FLAG_CHECKED the call returns RB_MISMATCHED_CHECKSUM if any
+ * session has failed by its end.  Bookkeeping errors (RB_INVALID_REQUEST,
+ * RB_PREDICTION_THRESHOLD, RB_PANIC) stop the run; *ticks_done = completed ticks. */
 rb_status rb_run_ticks(rb_batch* b, int32_t n_ticks, const void* inputs, int64_t tick_stride_bytes,
                        int32_t on_device, int32_t* ticks_done);
 
@@ -153,9 +159,11 @@ int32_t rb_last_requests(const rb_batch* b, int32_t* kinds, int32_t* frames, int
  * RB_INVALID_REQUEST if no cell holds that frame.  Synchronises. */
 rb_status rb_read_cell(rb_batch* b, int32_t frame, void* images, uint64_t* checksums);
 
-/* The game's live state after the last advance (ex_game Game::game_state) and
- * its display checksum (Game::last_checksum, ex_game.rs:104-111).  Synchronises. */
-rb_status rb_read_live(rb_batch* b, void* images, uint64_t* display_checksums, int32_t* display_frame);
+/* The game's live state after the last advance (ex_game Game::game_state,
+ * images [S][rb_state_bytes]) and its display checksum with its frame
+ * (Game::last_checksum, ex_game.rs:104-111; [S] each; RB_NULL_FRAME for games
+ * without one).  A failed session reports the state it stopped at.  Synchronises. */
+rb_status rb_read_live(rb_batch* b, void* images, uint64_t* display_checksums, int32_t* display_frames);
 
 /* Desync report for the cell holding `frame` into device memory [S]
  * rb_checksum_report (the P2P ChecksumReport payload; multi-GPU allgather
@@ -172,9 +180,11 @@ rb_status rb_debug_corrupt_cell(rb_batch* b, int32_t session, int32_t frame, int
  * libm in the parity tests. */
 rb_status rb_debug_sincosf(int32_t device, const float* x, float* sin_out, float* cos_out, int64_t n);
 
-/* HIP event timing of the tick kernel over the batch's stream, for bench.py:
- * returns the summed milliseconds and the count of tick launches since the
- * last call, and resets them (requires rb_profile_enable(b, 1) first). */
+/* HIP event timing of the tick kernel on the batch's stream, for bench.py:
+ * rb_profile_enable(b, k) brackets every k-th single-tick launch (k <= 1:
+ * every 8th) and every fused rb_run_ticks launch with an event pair;
+ * rb_profile_take returns the summed milliseconds of the timed launches and
+ * the number of ticks they covered, and resets both. */
 rb_status rb_profile_enable(rb_batch* b, int32_t on);
 rb_status rb_profile_take(rb_batch* b, double* total_ms, int32_t* launches);
 

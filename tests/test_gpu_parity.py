@@ -21,10 +21,10 @@ ORC_GAME = {G.Game.EX_GAME: O.EX_GAME, G.Game.STUB: O.STUB, G.Game.STUB_ENUM: O.
             G.Game.STUB_RANDOM_CS: O.STUB_RANDOM_CS}
 
 
-def make_pair(game, S, P=2, W=8, cd=2, d=0, checked=True, seed=0):
+def make_pair(game, S, P=2, W=8, cd=2, d=0, checked=True, seed=0, lane_per_session=False):
     sess = (G.SessionBuilder(game, num_sessions=S).with_num_players(P).with_max_prediction_window(W)
             .with_check_distance(cd).with_input_delay(d).with_checked_mismatches(checked).with_seed(seed)
-            .start_synctest_session())
+            .with_lane_per_session(lane_per_session).start_synctest_session())
     orc = O.OracleBatch(ORC_GAME[game], P, W, cd, d, S, seed)
     return sess, orc
 
@@ -54,8 +54,8 @@ def compare_live(sess, orc, game):
         assert (ofr == gfr).all()
 
 
-def run_parity(game, S, P, W, cd, d, T, inputs, check_every=1, checked=True):
-    sess, orc = make_pair(game, S, P, W, cd, d, checked)
+def run_parity(game, S, P, W, cd, d, T, inputs, check_every=1, checked=True, lane_per_session=False):
+    sess, orc = make_pair(game, S, P, W, cd, d, checked, lane_per_session=lane_per_session)
     for t in range(T):
         for h in range(P):
             sess.add_local_input(h, inputs[t, h])
@@ -97,10 +97,11 @@ def test_device_sincosf_bit_exact_with_glibc(gpu_available):
 # ---------------------------------------------------------------------------- ex_game
 @pytest.mark.parametrize("P,W,cd,d", [(2, 8, 7, 2), (2, 8, 2, 0), (2, 8, 0, 0), (2, 8, 1, 0), (1, 8, 3, 1),
                                       (3, 8, 5, 2), (4, 8, 7, 2), (2, 9, 8, 0), (2, 16, 12, 3)])
-def test_exgame_parity_every_tick(gpu_available, P, W, cd, d):
+@pytest.mark.parametrize("lane_per_session", [False, True], ids=["lane_per_player", "lane_per_session"])
+def test_exgame_parity_every_tick(gpu_available, P, W, cd, d, lane_per_session):
     S, T = 200, 70
     inputs = synth_inputs(S, P, T)
-    run_parity(G.Game.EX_GAME, S, P, W, cd, d, T, inputs)
+    run_parity(G.Game.EX_GAME, S, P, W, cd, d, T, inputs, lane_per_session=lane_per_session)
 
 
 def test_exgame_parity_long_run_periodic_and_wraparound(gpu_available):
@@ -135,6 +136,14 @@ def test_exgame_device_and_packed_inputs(gpu_available):
     compare_live(a, orc, G.Game.EX_GAME)
     compare_live(b, orc, G.Game.EX_GAME)
     compare_cells(b, orc, P, G.Game.EX_GAME)
+    # rb_run_ticks: the same T ticks in one native call, device and host inputs
+    c, _ = make_pair(G.Game.EX_GAME, S, P, 8, 7, 2)
+    assert c.run_ticks(dev) == T
+    compare_live(c, orc, G.Game.EX_GAME)
+    compare_cells(c, orc, P, G.Game.EX_GAME)
+    d, _ = make_pair(G.Game.EX_GAME, S, P, 8, 7, 2, checked=False)
+    assert d.run_ticks(inputs[:10]) == 10 and d.run_ticks(inputs[10:]) == T - 10
+    compare_live(d, orc, G.Game.EX_GAME)
 
 
 # ---------------------------------------------------------------------------- integer stubs: bit-exact checksums
@@ -235,7 +244,7 @@ def test_checksum_report_export(gpu_available):
     _, cs = sess.read_cell(f)
     np.testing.assert_array_equal(rep[:, 0], cs[:, 0])
     np.testing.assert_array_equal(rep[:, 1], cs[:, 1])
-    fr = rep[:, 2].view(np.int32).reshape(S, 2)
+    fr = np.ascontiguousarray(rep[:, 2]).view(np.int32).reshape(S, 2)
     assert (fr[:, 0] == f).all() and (fr[:, 1] == -1).all()
 
 
@@ -273,3 +282,67 @@ def test_bench_config_65536_sessions_sampled_parity(gpu_available):
         gi, gc = sess.read_cell(int(fr))
         np.testing.assert_array_equal(gi[sample], oc[w])
         np.testing.assert_array_equal(gc[sample], ocs[w])
+
+
+# ---------------------------------------------------------------------------- fused steady-state ticks (rb_run_ticks)
+@pytest.mark.parametrize("game,P,W,cd,d", [(G.Game.EX_GAME, 2, 8, 7, 2), (G.Game.EX_GAME, 2, 8, 1, 0),
+                                           (G.Game.EX_GAME, 1, 8, 4, 0), (G.Game.EX_GAME, 3, 6, 5, 1),
+                                           (G.Game.EX_GAME, 4, 9, 8, 3), (G.Game.EX_GAME, 2, 12, 11, 2),
+                                           (G.Game.STUB, 2, 8, 7, 2), (G.Game.STUB, 2, 8, 2, 0),
+                                           (G.Game.STUB_ENUM, 2, 8, 3, 1)])
+def test_run_ticks_fused_parity(gpu_available, game, P, W, cd, d):
+    """rb_run_ticks fuses consecutive steady-state ticks into one launch
+    (steady_kernel<G, CD>, CD <= 8; larger cd falls back to per-tick launches).
+    Chunks of ticks are compared bit-exactly with the oracle."""
+    import torch
+    S, T = 150, 120
+    mask, dtype = (0xFFFFFFFF, np.uint32) if game == G.Game.STUB else ((1, np.uint8) if game == G.Game.STUB_ENUM
+                                                                      else (0x0F, np.uint8))
+    inputs = synth_inputs(S, P, T, seed=77, mask=mask, dtype=dtype)
+    sess, orc = make_pair(game, S, P, W, cd, d)
+    dev = torch.from_numpy(inputs).cuda()
+    t = 0
+    for chunk in (3, 9, 1, 30, 13, 64):
+        n = min(chunk, T - t)
+        assert sess.run_ticks(dev[t:t + n]) == n
+        for k in range(t, t + n):
+            for h in range(P):
+                orc.add_local_input(h, inputs[k, h])
+            kinds, _ = orc.advance()
+            assert (kinds == 0).all()
+        t += n
+        assert [(int(r.kind), r.frame) for r in sess.last_requests()] == orc.trace(0)
+        compare_cells(sess, orc, P, game)
+        compare_live(sess, orc, game)
+    assert t == T
+
+
+def test_run_ticks_fused_mismatch_and_corruption(gpu_available):
+    """Mismatches detected inside a fused launch freeze exactly the sessions
+    (and report exactly the frames) that per-tick execution reports."""
+    import torch
+    S, P, cd = 64, 2, 7
+    inputs = synth_inputs(S, P, 60, seed=4)
+    sess, orc = make_pair(G.Game.EX_GAME, S, P, 8, cd, 2, checked=True)
+    dev = torch.from_numpy(inputs).cuda()
+    sess.run_ticks(dev[:20])
+    for k in range(20):
+        for h in range(P):
+            orc.add_local_input(h, inputs[k, h])
+        orc.advance()
+    f = sess.current_frame() - cd
+    for v in (5, 33):
+        sess.debug_corrupt_cell(v, f, 8 if v == 5 else 1, 0x10)
+        orc.corrupt_cell(v, f, 8 if v == 5 else 1, 0x10)
+    with pytest.raises(G.MismatchedChecksum) as ei:
+        sess.run_ticks(dev[20:60])
+    last_frames = None
+    for k in range(20, 60):
+        for h in range(P):
+            orc.add_local_input(h, inputs[k, h])
+        kinds, frames = orc.advance()
+        if (kinds != 0).any():
+            last_frames = np.where(kinds == 3, frames, -1)
+    np.testing.assert_array_equal(ei.value.frames, last_frames)
+    assert list(np.nonzero(ei.value.frames != -1)[0]) == [5, 33]
+    compare_live(sess, orc, G.Game.EX_GAME)
