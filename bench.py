@@ -50,8 +50,10 @@ def cpu_baseline(args, P):
 
 
 def pmc_traffic(cfg_key):
-    """HBM bytes per tick launch from the committed rocprofv3 PMC summary of this
-    exact configuration (profiles/*pmc*.json, written by tools/pmc_summary.py), or None."""
+    """HBM bytes per steady-state tick (all sessions) from the committed rocprofv3
+    PMC summary of this exact configuration (profiles/*pmc*.json, written by
+    tools/pmc_summary.py: FETCH_SIZE x2 + WRITE_SIZE per the gfx950 correction
+    in MI355X_MICROARCH.md), or None."""
     import glob
     best = None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
@@ -59,8 +61,8 @@ def pmc_traffic(cfg_key):
             d = json.load(open(path))
         except Exception:
             continue
-        if d.get("config_key") == cfg_key and d.get("hbm_bytes_per_launch"):
-            best = d["hbm_bytes_per_launch"]
+        if d.get("config_key") == cfg_key and d.get("hbm_bytes_per_tick"):
+            best = d["hbm_bytes_per_tick"]
     return best
 
 
@@ -77,8 +79,10 @@ def main():
     ap.add_argument("--seed", type=int, default=0x67677273)
     ap.add_argument("--report-interval", type=int, default=100,
                     help="ticks between RCCL all-gathers of desync reports (N>1); 0 = never")
-    ap.add_argument("--cpu-sessions", type=int, default=16384)
-    ap.add_argument("--cpu-ticks", type=int, default=32)
+    ap.add_argument("--ticks-per-launch", type=int, default=50,
+                    help="steady-state ticks fused into one steady_kernel launch (rb_run_ticks call)")
+    ap.add_argument("--cpu-sessions", type=int, default=65536)
+    ap.add_argument("--cpu-ticks", type=int, default=384)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--block-size", type=int, default=0)
     args = ap.parse_args()
@@ -117,21 +121,30 @@ def main():
     desyncs = torch.zeros((), dtype=torch.int64, device=dev)
 
     def run(t0, t1):
-        """Ticks [t0, t1): native multi-tick calls between desync-report points."""
-        t = t0
+        """Ticks [t0, t1): native multi-tick calls of at most --ticks-per-launch
+        ticks (one steady_kernel launch each once past the first cd+1 ticks),
+        split further at desync-report points."""
+        t, steady_launches = t0, 0
         while t < t1:
-            n = t1 - t
+            n = min(t1 - t, args.ticks_per_launch)
+            steady = sess.current_frame() > cd
+            if not steady:  # start-up ticks: per-tick launches, then align the steady chunks
+                n = min(n, cd + 1 - sess.current_frame())
             if world > 1 and args.report_interval:
                 to_report = args.report_interval - sess.current_frame() % args.report_interval
                 n = min(n, to_report)
             sess.run_ticks(dinputs[t:t + n])
+            steady_launches += steady
             t += n
             if world > 1 and args.report_interval and sess.current_frame() % args.report_interval == 0:
                 f = sess.current_frame() - 1
                 sess.export_checksum_report(f, reports.data_ptr())
                 dist.all_gather_into_tensor(gathered, reports)  # RCCL allgather of desync reports
                 desyncs.add_(((gathered[:, 2] >> 32) != -1).sum())  # mismatch_frame != NULL_FRAME
+        return steady_launches
 
+    if args.warmup < cd + 1:
+        raise SystemExit(f"--warmup must cover the {cd + 1} start-up ticks so the timed region is steady state")
     with torch.cuda.stream(stream):
         run(0, args.warmup)
         torch.cuda.synchronize()
@@ -141,13 +154,13 @@ def main():
         sess.profile_enable(True)
         sess.profile_take()
         t0 = time.perf_counter()
-        run(args.warmup, T)
+        launches = run(args.warmup, T)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
-        kernel_ms, launches = sess.profile_take()
+        kernel_ms, timed_ticks = sess.profile_take()  # HIP events around every steady_kernel launch
 
     nfail = int((sess.mismatches() != G.NULL_FRAME).sum())
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -161,13 +174,16 @@ def main():
         frames_per_tick = cd + 1
         total = S * world * frames_per_tick * args.steps
         value = total / elapsed
-        avg_kernel_s = kernel_ms / 1e3 / max(1, launches)
+        assert timed_ticks == args.steps, (timed_ticks, args.steps)
+        avg_kernel_s = kernel_ms / 1e3 / max(1, launches)  # per steady_kernel launch
+        ticks_per_launch = timed_ticks / max(1, launches)
         bpt = algorithmic_bytes_per_session_tick(P, cd, nw=5 * P, cs_bytes=2, in_rec=2 if P == 2 else (1 if P == 1 else 4),
                                                  in_bytes=1)
-        bytes_per_launch = bpt * S
+        bytes_per_launch = bpt * S * ticks_per_launch
         achieved = bytes_per_launch / avg_kernel_s / 1e9
         cfg_key = f"ex_game P={P} cd={cd} W={args.max_prediction} d={args.input_delay} S={S}"
-        traffic = pmc_traffic(cfg_key)
+        per_tick = pmc_traffic(cfg_key)
+        traffic = per_tick * ticks_per_launch if per_tick else None
         line = {
             "metric": METRIC,
             "value": value,
@@ -203,7 +219,10 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "algorithmic_bytes_per_launch": bytes_per_launch,
+                "algorithmic_bytes_per_session_tick": bpt,
                 "kernel_avg_us": avg_kernel_s * 1e6,
+                "ticks_per_launch": ticks_per_launch,
+                "launches_timed": launches,
                 "kernel": f"steady_kernel<ExGame<{P},true>,{cd}> (fused steady-state ticks)",
             },
             "cpu_baseline": None,
