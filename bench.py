@@ -92,6 +92,7 @@ def main():
     import torch.distributed as dist
 
     import ggrs_amd as G
+    from ggrs_amd import shard
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -107,8 +108,9 @@ def main():
     S = args.sessions_per_gpu
     T = args.warmup + args.steps
     # This rank's shard: global sessions [rank*S, (rank+1)*S); inputs keyed by global id.
-    inputs = G.synth_inputs(S * world, P, T, seed=args.seed)[:, :, rank * S:(rank + 1) * S]
-    dinputs = torch.from_numpy(np.ascontiguousarray(inputs)).to(dev)  # [T, P, S] u8, resident in HBM
+    lo, hi = shard.shard_range(rank, world, S * world)
+    inputs = G.synth_inputs(hi - lo, P, T, seed=args.seed, first_session=lo)
+    dinputs = torch.from_numpy(inputs).to(dev)  # [T, P, S] u8, resident in HBM
 
     stream = torch.cuda.Stream(device=dev)
     sess = (G.SessionBuilder(G.Game.EX_GAME, num_sessions=S, device=local).with_num_players(P)
@@ -116,8 +118,7 @@ def main():
             .with_input_delay(args.input_delay).with_checked_mismatches(False)
             .with_block_size(args.block_size).start_synctest_session())
     sess.set_stream(stream)
-    reports = torch.zeros((S, 3), dtype=torch.int64, device=dev)  # rb_checksum_report, 24 B
-    gathered = torch.zeros((S * world, 3), dtype=torch.int64, device=dev) if world > 1 else None
+    reports = torch.zeros((S, shard.REPORT_WORDS), dtype=torch.int64, device=dev)  # rb_checksum_report, 24 B
     desyncs = torch.zeros((), dtype=torch.int64, device=dev)
 
     def run(t0, t1):
@@ -139,8 +140,8 @@ def main():
             if world > 1 and args.report_interval and sess.current_frame() % args.report_interval == 0:
                 f = sess.current_frame() - 1
                 sess.export_checksum_report(f, reports.data_ptr())
-                dist.all_gather_into_tensor(gathered, reports)  # RCCL allgather of desync reports
-                desyncs.add_(((gathered[:, 2] >> 32) != -1).sum())  # mismatch_frame != NULL_FRAME
+                gathered = shard.gather_reports(reports)  # RCCL all-gather of desync reports
+                desyncs.add_(shard.count_desynced(gathered))  # mismatch_frame != NULL_FRAME
         return steady_launches
 
     if args.warmup < cd + 1:

@@ -1,0 +1,66 @@
+"""Multi-GPU session sharding and the desync-report all-gather.
+
+Sessions are independent (no cross-session state anywhere in SyncLayer /
+SyncTestSession), so each rank owns a contiguous range of global session ids
+and runs its own batch with no data-path collective.  The only exchange is the
+per-session desync report that mirrors P2P ``ChecksumReport{checksum, frame}``
+(/root/reference/src/network/messages.rs:75-79) plus the session's
+``MismatchedChecksum`` flag, all-gathered every ``interval`` frames like
+``check_checksum_send_interval`` / ``compare_local_checksums_against_peers``
+(src/sessions/p2p_session.rs:873-928).  With the ``nccl`` backend this is one
+RCCL all-gather over xGMI; ``gloo`` serves the CPU tests.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+NULL_FRAME = -1
+
+# rb_checksum_report (include/ggrs_amd.h): u64 lo, u64 hi, i32 frame, i32 mismatch_frame = 24 B
+REPORT_DTYPE = np.dtype([("checksum_lo", "<u8"), ("checksum_hi", "<u8"), ("frame", "<i4"),
+                         ("mismatch_frame", "<i4")])
+REPORT_WORDS = REPORT_DTYPE.itemsize // 8  # as int64 words for collectives
+
+
+def shard_range(rank: int, world: int, total_sessions: int):
+    """Global session ids [lo, hi) owned by ``rank`` (contiguous, balanced)."""
+    if not 0 <= rank < world:
+        raise ValueError("rank out of range")
+    return total_sessions * rank // world, total_sessions * (rank + 1) // world
+
+
+def pack_reports(checksums_u128: np.ndarray, frame: int, mismatch_frames: np.ndarray) -> np.ndarray:
+    """Host-side construction of [S] reports (what rb_export_checksum_report writes
+    on the device): checksums [S, 2] u64 (lo, hi), mismatch frames [S] i32."""
+    r = np.zeros(mismatch_frames.shape[0], REPORT_DTYPE)
+    r["checksum_lo"] = checksums_u128[:, 0]
+    r["checksum_hi"] = checksums_u128[:, 1]
+    r["frame"] = frame
+    r["mismatch_frame"] = mismatch_frames
+    return r
+
+
+def gather_reports(local, group=None):
+    """All-gather [S, 3] int64 report tensors (one rb_checksum_report per row) from
+    every rank; returns [world * S, 3] in rank order (= global session order)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    out = torch.empty((world * local.shape[0], local.shape[1]), dtype=local.dtype, device=local.device)
+    if dist.get_backend(group) == "nccl":
+        dist.all_gather_into_tensor(out, local, group=group)  # RCCL all-gather over xGMI
+    else:
+        parts = list(out.chunk(world))
+        dist.all_gather(parts, local, group=group)
+        out = torch.cat(parts)
+    return out
+
+
+def desynced_sessions(gathered):
+    """Global ids of sessions whose report carries a mismatch frame (as a tensor)."""
+    mismatch = gathered[:, 2] >> 32  # high half of the last word = mismatch_frame (little endian)
+    return (mismatch != NULL_FRAME).nonzero().flatten()
+
+
+def count_desynced(gathered):
+    return ((gathered[:, 2] >> 32) != NULL_FRAME).sum()

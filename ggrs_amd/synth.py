@@ -24,10 +24,11 @@ def splitmix64(x: np.ndarray) -> np.ndarray:
 
 
 def synth_inputs(num_sessions: int, num_players: int, frames: int, seed: int = SEED, mask: int = 0x0F,
-                 first_frame: int = 0, dtype=np.uint8) -> np.ndarray:
-    """Inputs for frames [first_frame, first_frame + frames) as [frames, P, S]."""
+                 first_frame: int = 0, dtype=np.uint8, first_session: int = 0) -> np.ndarray:
+    """Inputs for frames [first_frame, first_frame + frames) of global sessions
+    [first_session, first_session + num_sessions) as [frames, P, S]."""
     S, P = num_sessions, num_players
-    s = np.arange(S, dtype=np.uint64)[None, :]
+    s = np.arange(first_session, first_session + S, dtype=np.uint64)[None, :]
     p = np.arange(P, dtype=np.uint64)[:, None]
     key = (s << np.uint64(20)) + (p << np.uint64(16))  # [P, S]
     out = np.empty((frames, P, S), dtype=dtype)

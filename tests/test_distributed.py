@@ -1,0 +1,119 @@
+"""N>1 path on CPU: world size 2 over gloo (the GPU runs use nccl = RCCL).
+
+Each rank owns a contiguous shard of global sessions (ggrs_amd.shard), drives
+its own batch with no data-path collective, and all-gathers the per-session
+desync reports (rb_checksum_report) every interval.  The CPU stand-in for a
+rank's device batch is the oracle (test infrastructure) for values and a
+plan-only product batch (device=-1) for the request stream; the gathered
+reports must equal a single-process run over every session, and a snapshot
+corrupted on rank 1 must be visible to rank 0 at its global session id.
+"""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import ggrs_amd as G
+from ggrs_amd import shard
+from oracle import oracle as O
+
+TOTAL, P, CD, DELAY, T, INTERVAL = 24, 2, 7, 2, 40, 10
+VICTIM = 17  # global session id, owned by rank 1
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _reports_for(orc, frame):
+    frames, _, _, cs = orc.read_cells()
+    w = int(np.nonzero(frames == frame)[0][0])
+    k, f = orc.last_errors
+    return shard.pack_reports(cs[w], frame, np.where(k == 3, f, -1).astype(np.int32))
+
+
+def _drive(orc, plan, inputs, t, victim_local):
+    if t == 15 and victim_local is not None:
+        f = orc.current_frame() - CD
+        orc.corrupt_cell(victim_local, f, 0, 0x100)
+    for h in range(P):
+        orc.add_local_input(h, inputs[t, h])
+        if plan is not None:
+            plan.add_local_input(h, inputs[t, h])
+    orc.last_errors = orc.advance()
+    if plan is not None:
+        reqs = plan.advance_frame()
+        if (orc.last_errors[0] == 0).all():
+            assert [(int(r.kind), r.frame) for r in reqs] == orc.trace(0)
+
+
+def _rank_main(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lo, hi = shard.shard_range(rank, world, TOTAL)
+        inputs = G.synth_inputs(hi - lo, P, T, first_session=lo)
+        full = G.synth_inputs(TOTAL, P, T)
+        assert np.array_equal(inputs, full[:, :, lo:hi])  # inputs keyed by global session id
+        orc = O.OracleBatch(O.EX_GAME, P, 8, CD, DELAY, hi - lo)
+        plan = (G.SessionBuilder(G.Game.EX_GAME, num_sessions=hi - lo, device=-1).with_num_players(P)
+                .with_check_distance(CD).with_input_delay(DELAY).start_synctest_session())
+        victim = VICTIM - lo if lo <= VICTIM < hi else None
+        gathered_all = []
+        for t in range(T):
+            _drive(orc, plan, inputs, t, victim)
+            if orc.current_frame() % INTERVAL == 0:
+                rep = _reports_for(orc, orc.current_frame() - 1)
+                local = torch.from_numpy(rep.view(np.int64).reshape(-1, shard.REPORT_WORDS).copy())
+                g = shard.gather_reports(local)
+                gathered_all.append(g.numpy())
+                bad = shard.desynced_sessions(g).tolist()
+                assert bad == ([VICTIM] if t >= 15 else []), (t, bad)
+        np.save(os.path.join(outdir, f"rank{rank}.npy"), np.stack(gathered_all))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_ranges_partition_the_batch():
+    for total, world in [(24, 2), (65536 * 8, 8), (10, 3), (1, 1)]:
+        rs = [shard.shard_range(r, world, total) for r in range(world)]
+        assert rs[0][0] == 0 and rs[-1][1] == total
+        assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
+    with pytest.raises(ValueError):
+        shard.shard_range(2, 2, 10)
+
+
+def test_report_layout_matches_abi():
+    from ggrs_amd import _lib as L
+    import ctypes
+    assert shard.REPORT_DTYPE.itemsize == ctypes.sizeof(L.RbChecksumReport) == 24
+    r = shard.pack_reports(np.array([[5, 7]], np.uint64), 42, np.array([-1], np.int32))
+    w = r.view(np.int64)
+    assert w[0] == 5 and w[1] == 7 and (w[2] >> 32) == -1 and (w[2] & 0xFFFFFFFF) == 42
+
+
+def test_two_rank_gloo_report_allgather_equals_single_process():
+    port = _free_port()
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_rank_main, args=(2, port, d), nprocs=2, join=True)
+        r0 = np.load(os.path.join(d, "rank0.npy"))
+        r1 = np.load(os.path.join(d, "rank1.npy"))
+    np.testing.assert_array_equal(r0, r1)  # every rank sees the same node-wide reports
+    # single process over all sessions
+    orc = O.OracleBatch(O.EX_GAME, P, 8, CD, DELAY, TOTAL)
+    inputs = G.synth_inputs(TOTAL, P, T)
+    ref = []
+    for t in range(T):
+        _drive(orc, None, inputs, t, VICTIM)
+        if orc.current_frame() % INTERVAL == 0:
+            ref.append(_reports_for(orc, orc.current_frame() - 1).view(np.int64).reshape(-1, shard.REPORT_WORDS))
+    np.testing.assert_array_equal(r0, np.stack(ref))
