@@ -11,6 +11,11 @@ scaling: sessions per GPU fixed), no data-path collective; every
 --report-interval ticks the per-session desync reports (checksum of the last
 settled frame + mismatch flag) are all-gathered over RCCL.
 
+--game brawler runs BASELINE configs[2] instead: the fixed-point 256-entity
+brawler (8 KiB of integer state per session, one wavefront per session),
+same session count and rollback shape; its snapshot ring (4 GiB at 65,536
+sessions) does not fit any cache, so it is the HBM-bound line.
+
 Prints ONE JSON line (rank 0).
 """
 import argparse
@@ -40,11 +45,15 @@ def cpu_baseline(args, P):
     from oracle import oracle as O
     threads = max(1, min(16, os.cpu_count() or 1))
     S, warm, ticks = args.cpu_sessions, 16, args.cpu_ticks
-    secs, nerr = O.bench_exgame(P, args.check_distance, args.input_delay, args.max_prediction, S, warm, ticks,
-                                threads, args.seed)
+    fn = O.bench_brawler if args.game == "brawler" else O.bench_exgame
+    if S is None:
+        S = 4096 if args.game == "brawler" else 65536
+    if ticks is None:
+        ticks = 256 if args.game == "brawler" else 384
+    secs, nerr = fn(P, args.check_distance, args.input_delay, args.max_prediction, S, warm, ticks, threads, args.seed)
     sf = S * ticks * (args.check_distance + 1)
     return {"value": sf / secs, "unit": "session-frames/s", "cores": threads, "kind": "port",
-            "sample": f"{S} ex_game sessions x {ticks} steady-state ticks ({sf} session-frames) of the C++ "
+            "sample": f"{S} {args.game} sessions x {ticks} steady-state ticks ({sf} session-frames) of the C++ "
                       f"line-faithful restatement (reference allocation pattern), {threads} host threads, "
                       f"{secs:.2f} s wall, {nerr} errors"}
 
@@ -81,8 +90,10 @@ def main():
                     help="ticks between RCCL all-gathers of desync reports (N>1); 0 = never")
     ap.add_argument("--ticks-per-launch", type=int, default=50,
                     help="steady-state ticks fused into one steady_kernel launch (rb_run_ticks call)")
-    ap.add_argument("--cpu-sessions", type=int, default=65536)
-    ap.add_argument("--cpu-ticks", type=int, default=384)
+    ap.add_argument("--game", choices=["ex_game", "brawler"], default="ex_game",
+                    help="ex_game = BASELINE configs[1] (default); brawler = configs[2]")
+    ap.add_argument("--cpu-sessions", type=int, default=None)
+    ap.add_argument("--cpu-ticks", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--block-size", type=int, default=0)
     args = ap.parse_args()
@@ -109,11 +120,13 @@ def main():
     T = args.warmup + args.steps
     # This rank's shard: global sessions [rank*S, (rank+1)*S); inputs keyed by global id.
     lo, hi = shard.shard_range(rank, world, S * world)
-    inputs = G.synth_inputs(hi - lo, P, T, seed=args.seed, first_session=lo)
+    brawler = args.game == "brawler"
+    inputs = G.synth_inputs(hi - lo, P, T, seed=args.seed, first_session=lo, mask=0xFF if brawler else 0x0F)
     dinputs = torch.from_numpy(inputs).to(dev)  # [T, P, S] u8, resident in HBM
 
     stream = torch.cuda.Stream(device=dev)
-    sess = (G.SessionBuilder(G.Game.EX_GAME, num_sessions=S, device=local).with_num_players(P)
+    game = G.Game.BRAWLER if brawler else G.Game.EX_GAME
+    sess = (G.SessionBuilder(game, num_sessions=S, device=local).with_num_players(P)
             .with_max_prediction_window(args.max_prediction).with_check_distance(cd)
             .with_input_delay(args.input_delay).with_checked_mismatches(False)
             .with_block_size(args.block_size).start_synctest_session())
@@ -178,11 +191,16 @@ def main():
         assert timed_ticks == args.steps, (timed_ticks, args.steps)
         avg_kernel_s = kernel_ms / 1e3 / max(1, launches)  # per steady_kernel launch
         ticks_per_launch = timed_ticks / max(1, launches)
-        bpt = algorithmic_bytes_per_session_tick(P, cd, nw=5 * P, cs_bytes=2, in_rec=2 if P == 2 else (1 if P == 1 else 4),
-                                                 in_bytes=1)
+        in_rec = 2 if P == 2 else (1 if P == 1 else 4)
+        # device words of one session's state: ex_game 5 f32 per player (frame
+        # word implicit); brawler 256 entities x 8 i32
+        nw = 256 * 8 if brawler else 5 * P
+        bpt = algorithmic_bytes_per_session_tick(P, cd, nw=nw, cs_bytes=2, in_rec=in_rec, in_bytes=1)
+        if brawler:
+            bpt -= 2  # no display checksum (ex_game's Game::last_checksum only)
         bytes_per_launch = bpt * S * ticks_per_launch
         achieved = bytes_per_launch / avg_kernel_s / 1e9
-        cfg_key = f"ex_game P={P} cd={cd} W={args.max_prediction} d={args.input_delay} S={S}"
+        cfg_key = f"{args.game} P={P} cd={cd} W={args.max_prediction} d={args.input_delay} S={S}"
         per_tick = pmc_traffic(cfg_key)
         traffic = per_tick * ticks_per_launch if per_tick else None
         line = {
@@ -196,10 +214,12 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "i32" if brawler else "f32",
             "data": "synthetic",
             "config": {
-                "workload": f"ex_game SyncTestSession x {S} sessions/GPU ({S * world} total), 2 players, "
+                "workload": (f"fixed-point 256-entity brawler (8 KiB i32 state) SyncTestSession"
+                             if brawler else "ex_game SyncTestSession")
+                            + f" x {S} sessions/GPU ({S * world} total), {P} players, "
                             f"check_distance {cd} (8-frame rollback), input delay {args.input_delay}",
                 "sessions_per_gpu": S,
                 "total_sessions": S * world,
@@ -224,7 +244,8 @@ def main():
                 "kernel_avg_us": avg_kernel_s * 1e6,
                 "ticks_per_launch": ticks_per_launch,
                 "launches_timed": launches,
-                "kernel": f"steady_kernel<ExGame<{P},true>,{cd}> (fused steady-state ticks)",
+                "kernel": (f"steady_kernel<Brawler<{P}>,{cd}>" if brawler else f"steady_kernel<ExGame<{P},true>,{cd}>")
+                          + " (fused steady-state ticks)",
             },
             "cpu_baseline": None,
         }

@@ -30,6 +30,7 @@ RB_GAME_EX_GAME = 1
 RB_GAME_STUB = 2
 RB_GAME_STUB_ENUM = 3
 RB_GAME_STUB_RANDOM_CS = 4
+RB_GAME_BRAWLER = 5
 
 RB_FLAG_CHECKED = 1
 RB_FLAG_LANE_PER_SESSION = 2

@@ -522,6 +522,14 @@ inline std::unique_ptr<GameOps> make_game(int game, int players, bool lane_per_s
     case RB_GAME_STUB: return players == 2 ? std::make_unique<GameOpsT<StubGame>>() : nullptr;
     case RB_GAME_STUB_ENUM: return players == 2 ? std::make_unique<GameOpsT<StubEnumGame>>() : nullptr;
     case RB_GAME_STUB_RANDOM_CS: return players == 2 ? std::make_unique<GameOpsT<StubRandomCsGame>>() : nullptr;
+    case RB_GAME_BRAWLER:
+      switch (players) {
+        case 1: return std::make_unique<GameOpsT<Brawler<1>>>();
+        case 2: return std::make_unique<GameOpsT<Brawler<2>>>();
+        case 3: return std::make_unique<GameOpsT<Brawler<3>>>();
+        case 4: return std::make_unique<GameOpsT<Brawler<4>>>();
+        default: return nullptr;
+      }
     default: return nullptr;
   }
 }
@@ -718,14 +726,16 @@ rb_status rb_synctest_create(const rb_config* cfg, rb_batch** out) {
     return fail(nullptr, RB_INVALID_REQUEST, "negative or zero size in rb_config");
   // builder.rs:342-347
   if (cfg->check_distance >= cfg->max_prediction) return fail(nullptr, RB_INVALID_REQUEST, "Check distance too big.");
-  if (static_cast<uint64_t>(cfg->max_prediction) * 80 * ((static_cast<uint64_t>(cfg->num_sessions) + 63) / 64 * 64) >= (1ull << 32))
-    return fail(nullptr, RB_INVALID_REQUEST, "batch too large for 32-bit snapshot offsets");
   if (cfg->max_prediction > kMaxSteps)
     return fail(nullptr, RB_INVALID_REQUEST, "max_prediction above 64 is not supported by the device batch");
   if (cfg->input_delay > kQueueLen - cfg->max_prediction - 2)
     return fail(nullptr, RB_INVALID_REQUEST, "input delay does not fit the 128-entry input queue");
   auto ops = make_game(cfg->game, cfg->num_players, (cfg->flags & RB_FLAG_LANE_PER_SESSION) != 0);
   if (!ops) return fail(nullptr, RB_INVALID_REQUEST, "unsupported game / num_players combination");
+  // every snapshot word offset (slot * NW * lanes * Spad + ...) is 32-bit inside the kernels
+  if (static_cast<uint64_t>(cfg->max_prediction) * ops->nw * ops->lanes *
+          ((static_cast<uint64_t>(cfg->num_sessions) + 63) / 64 * 64) >= (1ull << 32))
+    return fail(nullptr, RB_INVALID_REQUEST, "batch too large for 32-bit snapshot offsets");
 
   auto b = std::make_unique<rb_batch>();
   b->cfg = *cfg;

@@ -212,6 +212,180 @@ struct ExGame {
   }
 };
 
+// Sum of a u32 over the 64 lanes of a wave (butterfly over ds_swizzle/bpermute);
+// every lane receives the total.
+__device__ __forceinline__ uint32_t wave_sum64(uint32_t v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), m, 64));
+  return v;
+}
+
+// ============================================================================
+// BASELINE config 3: fixed-point 256-entity brawler (no reference game; the
+// definition is oracle/ggrs_oracle.hpp namespace brawler, restated here).
+// One wavefront per session: lane l holds entities l, 64+l, 128+l, 192+l
+// (8 words each, 32 VGPRs); the players are entities 0..P-1 = lanes 0..P-1.
+// ============================================================================
+template <int P>
+struct Brawler {
+  static_assert(P >= 1 && P <= 4, "brawler supports 1..4 players");
+  static constexpr int kPlayers = P;
+  static constexpr int kLanes = 64;
+  static constexpr int kEntities = 256, kEntPerLane = 4;
+  static constexpr int NWL = 8 * kEntPerLane;
+  static constexpr int kInputBytes = 1;
+  static constexpr int kImageBytes = 4 + kEntities * 32;  // le32 frame || entities
+  static constexpr bool kDisplay = false;
+  static constexpr int kCanonWords = kEntities * 8;
+  using InRec = typename InRecOf<P>::T;
+  using CS = uint16_t;
+
+  static constexpr int32_t kArena = 1 << 20;
+  static constexpr int32_t kPlayerAcc = 1 << 12, kPlayerVmax = 1 << 14;
+  static constexpr int32_t kAiAcc = 1 << 10, kAiVmax = 1 << 13;
+  static constexpr int32_t kContact = 1 << 14;
+  static constexpr int32_t kAttackCd = 8, kAiDamage = 25, kPlayerHp0 = 1000, kAiHp0 = 100;
+  static constexpr uint64_t kInitKey = 0x627261776C6572ULL;
+  enum { X = 0, Y, VX, VY, HP, FLAGS, RNG, COUNTER };
+
+  // State::make (oracle brawler::State::make); words [64 lanes][32]
+  static void init(uint32_t* words) {
+    for (int e = 0; e < kEntities; ++e) {
+      const uint64_t h = splitmix64(kInitKey ^ static_cast<uint64_t>(e));
+      uint32_t* w = words + (e % 64) * NWL + (e / 64) * 8;
+      w[X] = static_cast<uint32_t>(h & (kArena - 1));
+      w[Y] = static_cast<uint32_t>((h >> 20) & (kArena - 1));
+      w[VX] = w[VY] = 0;
+      w[HP] = static_cast<uint32_t>(e < P ? kPlayerHp0 : kAiHp0);
+      w[FLAGS] = static_cast<uint32_t>(e < P ? 0 : e % P);
+      w[RNG] = static_cast<uint32_t>(h >> 32) | 1u;
+      w[COUNTER] = 0;
+    }
+  }
+  static void image(const uint32_t* words, int32_t frame, uint8_t* out) {
+    std::memcpy(out, &frame, 4);
+    for (int e = 0; e < kEntities; ++e) std::memcpy(out + 4 + 32 * e, words + (e % 64) * NWL + (e / 64) * 8, 32);
+  }
+  static void word_loc(int k, int* lane, int* word) {
+    const int e = k / 8, f = k % 8;
+    *lane = e % 64;
+    *word = (e / 64) * 8 + f;
+  }
+
+  __device__ static int32_t clampi(int32_t v, int32_t lo, int32_t hi) { return v < lo ? lo : (v > hi ? hi : v); }
+  __device__ static int32_t sgn(int32_t v) { return (v > 0) - (v < 0); }
+  __device__ static int32_t iabs(int32_t v) { return v < 0 ? -v : v; }
+  template <class T>
+  __device__ static T pick(const T (&a)[P], int32_t t) {  // a[t] for a per-lane t < P, no scratch
+    T r = a[0];
+#pragma unroll
+    for (int i = 1; i < P; ++i) r = t == i ? a[i] : r;
+    return r;
+  }
+
+  // State::advance (oracle brawler::State::advance): players, then AI against
+  // the players' new positions, then the damage the players took.
+  __device__ static void advance(uint32_t (&w)[NWL], InRec rec, int lane, uint32_t disc, uint32_t*) {
+    if (lane < P) {  // phase 1: player `lane` (entity lane, slot 0)
+      const uint32_t in = ((disc >> lane) & 1u) ? 0u : (static_cast<uint32_t>(rec) >> (8 * lane)) & 0xFFu;
+      const int32_t ax = static_cast<int32_t>((in >> 3) & 1u) - static_cast<int32_t>((in >> 2) & 1u);
+      const int32_t ay = static_cast<int32_t>((in >> 1) & 1u) - static_cast<int32_t>(in & 1u);
+      int32_t vx = static_cast<int32_t>(w[VX]), vy = static_cast<int32_t>(w[VY]);
+      vx = clampi(vx - (vx >> 3) + ax * kPlayerAcc, -kPlayerVmax, kPlayerVmax);
+      vy = clampi(vy - (vy >> 3) + ay * kPlayerAcc, -kPlayerVmax, kPlayerVmax);
+      w[VX] = static_cast<uint32_t>(vx);
+      w[VY] = static_cast<uint32_t>(vy);
+      w[X] = static_cast<uint32_t>(clampi(static_cast<int32_t>(w[X]) + vx, 0, kArena - 1));
+      w[Y] = static_cast<uint32_t>(clampi(static_cast<int32_t>(w[Y]) + vy, 0, kArena - 1));
+      int32_t cd = static_cast<int32_t>(w[FLAGS] & 0xFFu), atk = 0;
+      if ((in & 16u) && cd == 0) {
+        cd = kAttackCd;
+        atk = 1;
+      } else {
+        cd = cd > 0 ? cd - 1 : 0;
+      }
+      w[FLAGS] = static_cast<uint32_t>(cd | (atk << 8));
+    }
+    int32_t px[P], py[P], pa[P];
+#pragma unroll
+    for (int t = 0; t < P; ++t) {  // scalar broadcasts of the players' new state
+      px[t] = __builtin_amdgcn_readlane(static_cast<int>(w[X]), t);
+      py[t] = __builtin_amdgcn_readlane(static_cast<int>(w[Y]), t);
+      pa[t] = (__builtin_amdgcn_readlane(static_cast<int>(w[FLAGS]), t) >> 8) & 1;
+    }
+    uint32_t hits = 0;  // 8-bit count per player (at most 255 AI entities)
+#pragma unroll
+    for (int j = 0; j < kEntPerLane; ++j) {  // phase 2: AI entities j*64 + lane
+      uint32_t* q = &w[8 * j];
+      const bool ai = j > 0 || lane >= P;
+      if (!ai || static_cast<int32_t>(q[HP]) <= 0) continue;
+      const int32_t t = static_cast<int32_t>(q[FLAGS]);
+      const int32_t tx = pick(px, t), ty = pick(py, t), ta = pick(pa, t);
+      uint32_t r = q[RNG];
+      r ^= r << 13;
+      r ^= r >> 17;
+      r ^= r << 5;
+      q[RNG] = r;
+      const int32_t jx = static_cast<int32_t>(r & 0xFFu) - 128, jy = static_cast<int32_t>((r >> 8) & 0xFFu) - 128;
+      int32_t x = static_cast<int32_t>(q[X]), y = static_cast<int32_t>(q[Y]);
+      int32_t vx = static_cast<int32_t>(q[VX]), vy = static_cast<int32_t>(q[VY]);
+      vx = clampi(vx - (vx >> 2) + sgn(tx - x) * kAiAcc + jx, -kAiVmax, kAiVmax);
+      vy = clampi(vy - (vy >> 2) + sgn(ty - y) * kAiAcc + jy, -kAiVmax, kAiVmax);
+      x = clampi(x + vx, 0, kArena - 1);
+      y = clampi(y + vy, 0, kArena - 1);
+      q[X] = static_cast<uint32_t>(x);
+      q[Y] = static_cast<uint32_t>(y);
+      q[VX] = static_cast<uint32_t>(vx);
+      q[VY] = static_cast<uint32_t>(vy);
+      q[COUNTER] += 1u;
+      if (iabs(tx - x) + iabs(ty - y) < kContact) {
+        if (ta) {
+          const int32_t hp = static_cast<int32_t>(q[HP]) - kAiDamage;
+          q[HP] = static_cast<uint32_t>(hp < 0 ? 0 : hp);
+        } else {
+          hits += 1u << (8 * t);
+        }
+      }
+    }
+    hits = wave_sum64(hits);
+    if (lane < P) {  // phase 3
+      const int32_t dmg = static_cast<int32_t>((hits >> (8 * lane)) & 0xFFu);
+      const int32_t hp = static_cast<int32_t>(w[HP]) - dmg;
+      w[HP] = static_cast<uint32_t>(hp < 0 ? 0 : hp);
+      w[COUNTER] += static_cast<uint32_t>(dmg);
+    }
+  }
+
+  // fletcher16 of the 8196-byte image from registers: s1 = sum(b) mod 255,
+  // s2 = (n * sum(b) - sum(i * b)) mod 255.  Word f of entity e = j*64+lane sits
+  // at image offset o = 4 + 32e + 4f = (4 + 2048j + 4f) + 32*lane; per word two
+  // v_dot4_u32_u8 give its byte sum and sum(byte index * byte); per-lane sums are
+  // reduced mod 255 and packed before one wave butterfly.
+  __device__ static CS checksum(const uint32_t (&w)[NWL], int32_t frame, int lane, const CsCtx&) {
+    uint32_t sb = 0, sib = 0;
+#pragma unroll
+    for (int j = 0; j < kEntPerLane; ++j)
+#pragma unroll
+      for (int f = 0; f < 8; ++f) {
+        const uint32_t v = w[8 * j + f];
+        const uint32_t bs = __builtin_amdgcn_udot4(v, 0x01010101u, 0u, false);
+        sb += bs;
+        sib = __builtin_amdgcn_udot4(v, 0x03020100u, sib, false) + static_cast<uint32_t>(4 + 2048 * j + 4 * f) * bs;
+      }
+    sib += 32u * static_cast<uint32_t>(lane) * sb;
+    if (lane == 0) {  // frame word at offset 0
+      const uint32_t fr = static_cast<uint32_t>(frame);
+      sb = __builtin_amdgcn_udot4(fr, 0x01010101u, sb, false);
+      sib = __builtin_amdgcn_udot4(fr, 0x03020100u, sib, false);
+    }
+    const uint32_t tot = wave_sum64(((sib % 255u) << 16) | (sb % 255u));
+    const uint32_t s1 = (tot & 0xFFFFu) % 255u, b = (tot >> 16) % 255u;
+    constexpr uint32_t n_mod = static_cast<uint32_t>(kImageBytes) % 255u;
+    const uint32_t s2 = (n_mod * s1 + 255u - b) % 255u;
+    return static_cast<CS>((s2 << 8) | s1);
+  }
+};
+
 // ============================================================================
 // tests/stubs.rs GameStub / StateStub
 // ============================================================================

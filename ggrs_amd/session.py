@@ -91,10 +91,11 @@ class Game(enum.IntEnum):
     STUB = L.RB_GAME_STUB
     STUB_ENUM = L.RB_GAME_STUB_ENUM
     STUB_RANDOM_CS = L.RB_GAME_STUB_RANDOM_CS
+    BRAWLER = L.RB_GAME_BRAWLER
 
 
 INPUT_DTYPE = {Game.EX_GAME: np.uint8, Game.STUB: np.uint32, Game.STUB_ENUM: np.uint8,
-               Game.STUB_RANDOM_CS: np.uint32}
+               Game.STUB_RANDOM_CS: np.uint32, Game.BRAWLER: np.uint8}
 
 
 def _raise(lib, handle, status: int):

@@ -47,7 +47,9 @@ typedef enum rb_game {
   RB_GAME_EX_GAME = 1,        /* examples/ex_game/ex_game.rs: f32 ships, Input{inp:u8}, fletcher16 over the bincode image */
   RB_GAME_STUB = 2,           /* tests/stubs.rs GameStub: i32 state, StubInput{inp:u32}, SipHash-1-3 checksum */
   RB_GAME_STUB_ENUM = 3,      /* tests/stubs_enum.rs GameStubEnum: #[repr(u8)] enum input */
-  RB_GAME_STUB_RANDOM_CS = 4  /* tests/stubs.rs RandomChecksumGameStub: random u128 checksums (forces mismatches) */
+  RB_GAME_STUB_RANDOM_CS = 4, /* tests/stubs.rs RandomChecksumGameStub: random u128 checksums (forces mismatches) */
+  RB_GAME_BRAWLER = 5         /* BASELINE config 3: fixed-point 256-entity brawler, 8 KiB state, Input{inp:u8}, fletcher16;
+                                 no reference game exists: defined in oracle/ggrs_oracle.hpp */
 } rb_game;
 
 /* GGRSRequest kinds (lib.rs:170-194) for rb_last_requests. */

@@ -799,6 +799,156 @@ struct GameStubEnum {
 }  // namespace stub
 
 // ===========================================================================
+// BASELINE config 3: the fixed-point 256-entity brawler.  The reference has no
+// such game: this is the build's own definition, written
+// once here (sequential, entity-index order) and restated on the device
+// (ggrs_amd/csrc/games.hpp Brawler, one wavefront per session).  Parity is
+// between those two only; the request-stream semantics around it are the
+// reference's.  Integer-only, so checksums are bit-exact by construction.
+//
+// Entity e (8 x i32 = 32 B): x, y (Q16.16, arena [0, 2^20)), vx, vy, hp,
+// flags (players: cooldown | attacking << 8; AI: target player), rng
+// (xorshift32 state), counter (players: damage taken; AI: frames alive).
+// Entities 0..P-1 are the players.  Image = le32 frame || 256 x 8 x le32
+// (8196 B); checksum = fletcher16 of the image (as ex_game.rs:90-91).
+// ===========================================================================
+namespace brawler {
+constexpr int N = 256;
+constexpr int32_t ARENA = 1 << 20;
+constexpr int32_t PLAYER_ACC = 1 << 12, PLAYER_VMAX = 1 << 14;
+constexpr int32_t AI_ACC = 1 << 10, AI_VMAX = 1 << 13;
+constexpr int32_t CONTACT = 1 << 14;
+constexpr int32_t ATTACK_CD = 8, AI_DAMAGE = 25, PLAYER_HP0 = 1000, AI_HP0 = 100;
+constexpr uint64_t INIT_KEY = 0x627261776C6572ULL;  // "brawler"
+constexpr uint8_t IN_UP = 1, IN_DOWN = 2, IN_LEFT = 4, IN_RIGHT = 8, IN_ATTACK = 16;
+enum Word { X = 0, Y, VX, VY, HP, FLAGS, RNG, COUNTER };
+
+struct Input {
+  uint8_t inp = 0;
+};
+
+inline int32_t clamp(int32_t v, int32_t lo, int32_t hi) { return v < lo ? lo : (v > hi ? hi : v); }
+inline int32_t sgn(int32_t v) { return (v > 0) - (v < 0); }
+inline int32_t iabs(int32_t v) { return v < 0 ? -v : v; }
+
+inline uint64_t mix64(uint64_t x) {  // splitmix64
+  x += 0x9e3779b97f4a7c15ULL;
+  x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  x = (x ^ (x >> 27)) * 0x94d049bb133111ebULL;
+  return x ^ (x >> 31);
+}
+
+struct State {
+  int32_t frame = 0;
+  int32_t num_players = 0;
+  std::vector<int32_t> ent;  // [N][8], heap like ex_game's Vecs
+
+  static State make(int32_t P) {
+    State s;
+    s.num_players = P;
+    s.ent.assign(N * 8, 0);
+    for (int e = 0; e < N; ++e) {
+      const uint64_t h = mix64(INIT_KEY ^ static_cast<uint64_t>(e));
+      int32_t* w = &s.ent[e * 8];
+      w[X] = static_cast<int32_t>(h & (ARENA - 1));
+      w[Y] = static_cast<int32_t>((h >> 20) & (ARENA - 1));
+      w[HP] = e < P ? PLAYER_HP0 : AI_HP0;
+      w[FLAGS] = e < P ? 0 : e % P;
+      w[RNG] = static_cast<int32_t>(static_cast<uint32_t>(h >> 32) | 1u);
+    }
+    return s;
+  }
+
+  void advance(const std::vector<std::pair<Input, InputStatus>>& inputs) {
+    frame += 1;
+    const int P = num_players;
+    // phase 1: players
+    for (int e = 0; e < P; ++e) {
+      int32_t* w = &ent[e * 8];
+      const uint32_t in = inputs[e].second == InputStatus::Disconnected ? 0u : inputs[e].first.inp;
+      const int32_t ax = static_cast<int32_t>((in >> 3) & 1) - static_cast<int32_t>((in >> 2) & 1);
+      const int32_t ay = static_cast<int32_t>((in >> 1) & 1) - static_cast<int32_t>(in & 1);
+      w[VX] = clamp(w[VX] - (w[VX] >> 3) + ax * PLAYER_ACC, -PLAYER_VMAX, PLAYER_VMAX);
+      w[VY] = clamp(w[VY] - (w[VY] >> 3) + ay * PLAYER_ACC, -PLAYER_VMAX, PLAYER_VMAX);
+      w[X] = clamp(w[X] + w[VX], 0, ARENA - 1);
+      w[Y] = clamp(w[Y] + w[VY], 0, ARENA - 1);
+      int32_t cd = w[FLAGS] & 0xFF, atk = 0;
+      if ((in & IN_ATTACK) && cd == 0) {
+        cd = ATTACK_CD;
+        atk = 1;
+      } else {
+        cd = cd > 0 ? cd - 1 : 0;
+      }
+      w[FLAGS] = cd | (atk << 8);
+    }
+    // phase 2: AI entities chase their target player (new positions)
+    int32_t hits[4] = {0, 0, 0, 0};
+    for (int e = P; e < N; ++e) {
+      int32_t* w = &ent[e * 8];
+      if (w[HP] <= 0) continue;
+      const int t = w[FLAGS];
+      const int32_t* pw = &ent[t * 8];
+      uint32_t r = static_cast<uint32_t>(w[RNG]);
+      r ^= r << 13;
+      r ^= r >> 17;
+      r ^= r << 5;
+      w[RNG] = static_cast<int32_t>(r);
+      const int32_t jx = static_cast<int32_t>(r & 0xFF) - 128, jy = static_cast<int32_t>((r >> 8) & 0xFF) - 128;
+      w[VX] = clamp(w[VX] - (w[VX] >> 2) + sgn(pw[X] - w[X]) * AI_ACC + jx, -AI_VMAX, AI_VMAX);
+      w[VY] = clamp(w[VY] - (w[VY] >> 2) + sgn(pw[Y] - w[Y]) * AI_ACC + jy, -AI_VMAX, AI_VMAX);
+      w[X] = clamp(w[X] + w[VX], 0, ARENA - 1);
+      w[Y] = clamp(w[Y] + w[VY], 0, ARENA - 1);
+      w[COUNTER] += 1;
+      if (iabs(pw[X] - w[X]) + iabs(pw[Y] - w[Y]) < CONTACT) {
+        if ((pw[FLAGS] >> 8) & 1) {
+          w[HP] = std::max(w[HP] - AI_DAMAGE, 0);
+        } else {
+          hits[t] += 1;
+        }
+      }
+    }
+    // phase 3: damage to players
+    for (int e = 0; e < P; ++e) {
+      int32_t* w = &ent[e * 8];
+      w[HP] = std::max(w[HP] - hits[e], 0);
+      w[COUNTER] += hits[e];
+    }
+  }
+};
+
+inline std::vector<uint8_t> image(const State& s) {
+  std::vector<uint8_t> out(4 + s.ent.size() * 4);
+  std::memcpy(out.data(), &s.frame, 4);
+  std::memcpy(out.data() + 4, s.ent.data(), s.ent.size() * 4);
+  return out;
+}
+
+struct Config {
+  using Input = brawler::Input;
+  using State = brawler::State;
+};
+
+struct Game {
+  State gs;
+  explicit Game(int32_t P) : gs(State::make(P)) { ORC_ASSERT(P >= 1 && P <= 4); }
+  void handle_requests(std::vector<Request<Config>>& reqs) {
+    for (auto& r : reqs) {
+      switch (r.kind) {
+        case RequestKind::Load: { auto d = r.cell.load(); if (!d) throw Panic("No data found."); gs = *d; break; }
+        case RequestKind::Save: {
+          ORC_ASSERT(gs.frame == r.frame);
+          auto buf = image(gs);
+          r.cell.save(r.frame, gs, static_cast<u128>(fletcher16(buf.data(), buf.size())));
+          break;
+        }
+        case RequestKind::Advance: gs.advance(r.inputs); break;
+      }
+    }
+  }
+};
+}  // namespace brawler
+
+// ===========================================================================
 // Synthetic input generator — shared definition with
 // ggrs_amd/synth.py (tests check they agree).
 // ===========================================================================

@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
 REF_TESTS = os.path.join(_HERE, "build", "ref_tests")
 
-EX_GAME, STUB, STUB_ENUM, STUB_RANDOM_CS = 1, 2, 3, 4
+EX_GAME, STUB, STUB_ENUM, STUB_RANDOM_CS, BRAWLER = 1, 2, 3, 4, 5
 KIND_PANIC = 99
 _lib = None
 
@@ -50,6 +50,7 @@ def load():
             "orc_batch_corrupt_cell": (I32, [P, I32, I32, I32, ctypes.c_uint32]),
             "orc_synth_inputs": (None, [U64, ctypes.c_uint32, I32, I32, I32, I32, I32, P]),
             "orc_bench_exgame": (ctypes.c_double, [I32, I32, I32, I32, I32, I32, I32, I32, U64, PI32]),
+            "orc_bench_brawler": (ctypes.c_double, [I32, I32, I32, I32, I32, I32, I32, I32, U64, PI32]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
@@ -164,4 +165,13 @@ def bench_exgame(num_players: int, check_distance: int, input_delay: int, max_pr
     ne = ctypes.c_int32()
     t = load().orc_bench_exgame(num_players, check_distance, input_delay, max_prediction, sessions, warmup, ticks,
                                 threads, seed, ctypes.byref(ne))
+    return t, ne.value
+
+
+def bench_brawler(num_players: int, check_distance: int, input_delay: int, max_prediction: int, sessions: int,
+                  warmup: int, ticks: int, threads: int, seed: int):
+    """CPU 'port' baseline for the brawler (BASELINE config 3): wall seconds."""
+    ne = ctypes.c_int32()
+    t = load().orc_bench_brawler(num_players, check_distance, input_delay, max_prediction, sessions, warmup, ticks,
+                                 threads, seed, ctypes.byref(ne))
     return t, ne.value

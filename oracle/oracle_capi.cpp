@@ -18,7 +18,7 @@ using namespace orc;
 
 namespace {
 
-enum GameId : int32_t { EX_GAME = 1, STUB = 2, STUB_ENUM = 3, STUB_RANDOM_CS = 4 };
+enum GameId : int32_t { EX_GAME = 1, STUB = 2, STUB_ENUM = 3, STUB_RANDOM_CS = 4, BRAWLER = 5 };
 constexpr int32_t KIND_PANIC = 99;
 
 struct BatchBase {
@@ -47,6 +47,7 @@ inline std::vector<uint8_t> image_of(const stub::StateStubEnum& s) {
   std::memcpy(v.data() + 4, &s.state, 4);
   return v;
 }
+inline std::vector<uint8_t> image_of(const brawler::State& s) { return brawler::image(s); }
 inline uint64_t display_checksum(const exgame::Game& g, int32_t* f) { *f = g.last_checksum.first; return g.last_checksum.second; }
 template <class G>
 inline uint64_t display_checksum(const G&, int32_t* f) { *f = NULL_FRAME; return 0; }
@@ -63,6 +64,9 @@ inline void corrupt_state(exgame::State& st, int32_t k, uint32_t m) {
   std::memcpy(&u, f, 4);
   u ^= m;
   std::memcpy(f, &u, 4);
+}
+inline void corrupt_state(brawler::State& st, int32_t k, uint32_t m) {
+  st.ent.at(static_cast<size_t>(k)) ^= static_cast<int32_t>(m);  // canonical word k = entity * 8 + field
 }
 inline void corrupt_state(stub::StateStub& st, int32_t, uint32_t m) { st.state ^= static_cast<int32_t>(m); }
 inline void corrupt_state(stub::StateStubEnum& st, int32_t, uint32_t m) { st.state ^= static_cast<int32_t>(m); }
@@ -194,6 +198,7 @@ thread_local std::string g_err;
 extern "C" {
 
 int32_t orc_image_bytes(int32_t game, int32_t num_players) {
+  if (game == BRAWLER) return 4 + brawler::N * 32;
   return game == EX_GAME ? 36 + 20 * num_players : 8;
 }
 int32_t orc_input_bytes(int32_t game) { return (game == STUB || game == STUB_RANDOM_CS) ? 4 : 1; }
@@ -213,6 +218,8 @@ void* orc_batch_create(int32_t game, int32_t num_players, int32_t max_prediction
         return new Batch<stub::Config, stub::GameStub>(b, num_sessions, [&](int32_t) { return stub::GameStub{}; });
       case STUB_ENUM:
         return new Batch<stub::EnumConfig, stub::GameStubEnum>(b, num_sessions, [&](int32_t) { return stub::GameStubEnum{}; });
+      case BRAWLER:
+        return new Batch<brawler::Config, brawler::Game>(b, num_sessions, [&](int32_t) { return brawler::Game(num_players); });
       case STUB_RANDOM_CS:
         return new Batch<stub::Config, stub::RandomChecksumGameStub>(
             b, num_sessions, [&](int32_t s) { return stub::RandomChecksumGameStub(seed ^ (uint64_t(s) * 0x9e37ULL)); });
@@ -278,23 +285,26 @@ void orc_synth_inputs(uint64_t seed, uint32_t mask, int32_t S, int32_t P, int32_
       }
 }
 
-// CPU baseline ("port"): S independent ex_game SyncTest sessions driven exactly
-// like ex_game_synctest.rs:59-72 on `threads` host threads.  Inputs are
-// generated before the timed region (as on the GPU side).  Returns the wall
-// seconds of the `ticks` timed ticks (after `warmup` untimed ones); writes the
-// number of sessions that reported an error to *n_err.
-double orc_bench_exgame(int32_t num_players, int32_t check_distance, int32_t input_delay, int32_t max_prediction,
-                        int32_t S, int32_t warmup, int32_t ticks, int32_t threads, uint64_t seed, int32_t* n_err) {
+// CPU baseline ("port"): S independent SyncTest sessions of a u8-input game
+// driven exactly like ex_game_synctest.rs:59-72 on `threads` host threads.
+// Inputs are generated before the timed region (as on the GPU side).  Returns
+// the wall seconds of the `ticks` timed ticks (after `warmup` untimed ones);
+// writes the number of sessions that reported an error to *n_err.
+}  // extern "C"
+
+template <class Cfg, class Game>
+double bench_game(int32_t num_players, int32_t check_distance, int32_t input_delay, int32_t max_prediction, int32_t S,
+                  int32_t warmup, int32_t ticks, int32_t threads, uint64_t seed, uint32_t mask, int32_t* n_err) {
   SessionBuilder b;
   b.with_num_players(num_players).with_check_distance(check_distance).with_input_delay(input_delay);
   if (b.with_max_prediction_window(max_prediction).is_err()) return -1.0;
   const int32_t P = num_players, T = warmup + ticks;
   std::vector<uint8_t> in(static_cast<size_t>(T) * P * S);
-  orc_synth_inputs(seed, 0x0F, S, P, T, 0, 1, in.data());
+  orc_synth_inputs(seed, mask, S, P, T, 0, 1, in.data());
   if (threads < 1) threads = 1;
   struct Worker {
-    std::vector<std::unique_ptr<SyncTestSession<exgame::Config>>> sess;
-    std::vector<exgame::Game> games;
+    std::vector<std::unique_ptr<SyncTestSession<Cfg>>> sess;
+    std::vector<Game> games;
     int32_t s0 = 0, s1 = 0, errs = 0;
   };
   std::vector<Worker> ws(threads);
@@ -303,12 +313,12 @@ double orc_bench_exgame(int32_t num_players, int32_t check_distance, int32_t inp
     ws[t].s1 = static_cast<int32_t>(static_cast<int64_t>(S) * (t + 1) / threads);
   }
   auto run = [&](Worker& w, int32_t f0, int32_t f1) {
-    std::vector<Request<exgame::Config>> reqs;
+    std::vector<Request<Cfg>> reqs;
     for (int32_t f = f0; f < f1; ++f)
       for (int32_t s = w.s0; s < w.s1; ++s) {
         auto& sess = *w.sess[s - w.s0];
         for (int32_t p = 0; p < P; ++p)
-          sess.add_local_input(p, exgame::Input{in[(static_cast<size_t>(f) * P + p) * S + s]});
+          sess.add_local_input(p, typename Cfg::Input{in[(static_cast<size_t>(f) * P + p) * S + s]});
         Error e = sess.advance_frame(reqs);
         if (e.is_err()) { ++w.errs; continue; }
         w.games[s - w.s0].handle_requests(reqs);
@@ -321,8 +331,8 @@ double orc_bench_exgame(int32_t num_players, int32_t check_distance, int32_t inp
   };
   parallel([&](Worker& w) {
     for (int32_t s = w.s0; s < w.s1; ++s) {
-      std::unique_ptr<SyncTestSession<exgame::Config>> p;
-      b.start_synctest_session<exgame::Config>(&p);
+      std::unique_ptr<SyncTestSession<Cfg>> p;
+      b.start_synctest_session<Cfg>(&p);
       w.sess.push_back(std::move(p));
       w.games.emplace_back(num_players);
     }
@@ -335,6 +345,20 @@ double orc_bench_exgame(int32_t num_players, int32_t check_distance, int32_t inp
   for (auto& w : ws) e += w.errs;
   if (n_err) *n_err = e;
   return std::chrono::duration<double>(t1 - t0).count();
+}
+
+extern "C" {
+
+double orc_bench_exgame(int32_t num_players, int32_t check_distance, int32_t input_delay, int32_t max_prediction,
+                        int32_t S, int32_t warmup, int32_t ticks, int32_t threads, uint64_t seed, int32_t* n_err) {
+  return bench_game<exgame::Config, exgame::Game>(num_players, check_distance, input_delay, max_prediction, S, warmup,
+                                                  ticks, threads, seed, 0x0F, n_err);
+}
+
+double orc_bench_brawler(int32_t num_players, int32_t check_distance, int32_t input_delay, int32_t max_prediction,
+                         int32_t S, int32_t warmup, int32_t ticks, int32_t threads, uint64_t seed, int32_t* n_err) {
+  return bench_game<brawler::Config, brawler::Game>(num_players, check_distance, input_delay, max_prediction, S,
+                                                    warmup, ticks, threads, seed, 0xFF, n_err);
 }
 
 }  // extern "C"

@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 F32_RTOL = 1e-5  # north_star tolerance for f32 ex_game state
 
 ORC_GAME = {G.Game.EX_GAME: O.EX_GAME, G.Game.STUB: O.STUB, G.Game.STUB_ENUM: O.STUB_ENUM,
-            G.Game.STUB_RANDOM_CS: O.STUB_RANDOM_CS}
+            G.Game.STUB_RANDOM_CS: O.STUB_RANDOM_CS, G.Game.BRAWLER: O.BRAWLER}
 
 
 def make_pair(game, S, P=2, W=8, cd=2, d=0, checked=True, seed=0, lane_per_session=False):

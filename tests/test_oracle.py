@@ -98,3 +98,26 @@ def test_oracle_exgame_state_new_and_bincode_image():
     assert int.from_bytes(f[4:12].tobytes(), "little") == 2  # num_players
     pos = f[20:36].view(np.float32)
     assert np.allclose(pos, [450.0, 400.0, 150.0, 400.0], atol=1e-3)
+
+
+def test_oracle_brawler_synctest_runs_and_exercises_the_rules():
+    # BASELINE config 3 (no reference game; oracle/ggrs_oracle.hpp brawler):
+    # deterministic resimulation never mismatches, and over 300 frames the AI
+    # reaches the players (damage both ways), so every rule is exercised.
+    S, P, T = 12, 4, 300
+    inputs = synth_inputs(S, P, T, seed=5, mask=0x1F)
+    b = O.OracleBatch(O.BRAWLER, P, 8, 7, 2, S)
+    img, _, _ = b.read_live()
+    assert img.shape == (S, 4 + 256 * 32)
+    for t in range(T):
+        for h in range(P):
+            b.add_local_input(h, inputs[t, h])
+        k, _ = b.advance()
+        assert (k == 0).all(), t
+    img, _, _ = b.read_live()
+    ent = img[:, 4:].copy().view(np.int32).reshape(S, 256, 8)
+    assert (img[:, :4].copy().view(np.int32) == T).all()
+    assert (ent[:, :, 0] >= 0).all() and (ent[:, :, 0] < (1 << 20)).all()
+    assert (ent[:, :P, 7] > 0).any(), "no player took damage"
+    assert (ent[:, P:, 4] < 100).any(), "no AI entity took damage"
+    assert (ent[:, P:, 7] > 0).all() or (ent[:, P:, 4] <= 0).any()
