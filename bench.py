@@ -31,14 +31,18 @@ METRIC = "session-frames resimulated/sec (node) at 8-frame rollback; % HBM roofl
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
-def algorithmic_bytes_per_session_tick(P: int, cd: int, nw: int, cs_bytes: int, in_rec: int, in_bytes: int) -> int:
-    """Bytes one steady-state tick must move per session (DESIGN.md §Roofline):
-    1 snapshot load + cd snapshot saves, cd cell checksums written, cd-1
-    first-seen reads + 1 first-seen write, cd+1 input records read, the new
-    inputs read and written to the input ring, the display checksum written."""
+def algorithmic_bytes_per_session_tick(P: int, cd: int, nw: int, cs_bytes: int, in_rec: int, in_bytes: int,
+                                       display: bool = True) -> int:
+    """Bytes one steady-state tick must move per session (DESIGN.md §4):
+    1 snapshot load (LoadGameState) + cd snapshot saves, cd cell checksums
+    written, the first-seen record of frame c written, the tick's new inputs
+    read and written to the input ring, the input of the window's newest frame
+    read, and the display checksum written (ex_game).  First-seen values and
+    inputs of older frames are carried in registers across the fused ticks
+    (steady_kernel), so they are not counted."""
     state = 4 * nw
-    return (state * (1 + cd) + cs_bytes * cd + cs_bytes * (cd - 1) + cs_bytes + in_rec * (cd + 1)
-            + P * in_bytes + in_rec + cs_bytes)
+    return (state * (1 + cd) + cs_bytes * cd + cs_bytes + P * in_bytes + in_rec + P * in_bytes
+            + (cs_bytes if display else 0))
 
 
 def cpu_baseline(args, P):
@@ -195,9 +199,8 @@ def main():
         # device words of one session's state: ex_game 5 f32 per player (frame
         # word implicit); brawler 256 entities x 8 i32
         nw = 256 * 8 if brawler else 5 * P
-        bpt = algorithmic_bytes_per_session_tick(P, cd, nw=nw, cs_bytes=2, in_rec=in_rec, in_bytes=1)
-        if brawler:
-            bpt -= 2  # no display checksum (ex_game's Game::last_checksum only)
+        bpt = algorithmic_bytes_per_session_tick(P, cd, nw=nw, cs_bytes=2, in_rec=in_rec, in_bytes=1,
+                                                 display=not brawler)
         bytes_per_launch = bpt * S * ticks_per_launch
         achieved = bytes_per_launch / avg_kernel_s / 1e9
         cfg_key = f"{args.game} P={P} cd={cd} W={args.max_prediction} d={args.input_delay} S={S}"

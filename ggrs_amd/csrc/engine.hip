@@ -1,4 +1,7 @@
-// ggrs_amd/csrc/engine.hip — MI355X batched rollback-resimulation engine.
+// ggrs_amd/csrc/engine.hip — MI355X batched rollback-resimulation engine: host side
+// (rb_batch, the C ABI of include/ggrs_amd.h).  Kernels: kernels.hpp, instantiated
+// per game in ops_exgame.hip / ops_brawler.hip / ops_stub.hip.
+//
 //
 // One rb_batch = S independent SyncTestSessions in lock-step.  Per tick the
 // host mirror (planner.hpp) produces the reference's request stream and lowers
@@ -26,399 +29,9 @@
 #include <string>
 #include <vector>
 
-#include "../../include/ggrs_amd.h"
-#include "games.hpp"
-#include "planner.hpp"
+#include "kernels.hpp"
 
 namespace rb {
-
-constexpr int kChunk = 8;  // inputs prefetched per chunk of AdvanceFrames
-constexpr int kMaxRepl = 8;
-
-struct KParams {
-  uint32_t* snap;
-  uint32_t* live;
-  void* cs;
-  void* fs;
-  void* ring;
-  void* last_cs;
-  void* periodic_cs;
-  int32_t* err;
-  int32_t* live_frame;
-  unsigned long long* frozen;
-  uint32_t* counters;  // [0] sessions failed, [1] unexpected-path count
-  const void* in_ptr[4];
-  int32_t in_mode;  // 0: no new input, 1: one array per player, 2: packed [S][P]
-  int32_t S, Spad, W;
-  int32_t user_slot, n_repl, repl_src;
-  int32_t repl_dst[kMaxRepl];
-  int32_t load_slot;  // -1: start from the live state
-  int32_t f0, n_steps;
-  uint32_t save_modes[kMaxSteps / 16];  // 2 bits per step
-  int32_t slot0;                        // f0 % W (snapshot slot of step 0)
-  int32_t live_out, periodic_step, display;
-  uint32_t disc_mask;
-  uint64_t seed;
-  uint32_t nonce_base;
-  uint32_t debug;  // experiment knobs (rb_config.reserved[0]); 0 in every real run
-};
-
-// ---- SoA planes: word k of session s inside a block of NW planes -------------
-template <int NW>
-__device__ __forceinline__ void load_words(const uint32_t* __restrict__ base, int Spad, int s, uint32_t (&w)[NW]) {
-  constexpr int Q4 = NW / 4, R = NW % 4;
-#pragma unroll
-  for (int j = 0; j < Q4; ++j) {
-    const uint4 v = reinterpret_cast<const uint4*>(base + j * 4 * Spad)[s];
-    w[4 * j + 0] = v.x;
-    w[4 * j + 1] = v.y;
-    w[4 * j + 2] = v.z;
-    w[4 * j + 3] = v.w;
-  }
-  const uint32_t* b = base + Q4 * 4 * Spad;
-  if constexpr (R >= 2) {
-    const uint2 v = reinterpret_cast<const uint2*>(b)[s];
-    w[Q4 * 4 + 0] = v.x;
-    w[Q4 * 4 + 1] = v.y;
-    b += 2 * Spad;
-  }
-  if constexpr (R & 1) w[NW - 1] = b[s];
-}
-template <int NW>
-__device__ __forceinline__ void store_words(uint32_t* __restrict__ base, int Spad, int s, const uint32_t (&w)[NW]) {
-  constexpr int Q4 = NW / 4, R = NW % 4;
-#pragma unroll
-  for (int j = 0; j < Q4; ++j)
-    reinterpret_cast<uint4*>(base + j * 4 * Spad)[s] = make_uint4(w[4 * j], w[4 * j + 1], w[4 * j + 2], w[4 * j + 3]);
-  uint32_t* b = base + Q4 * 4 * Spad;
-  if constexpr (R >= 2) {
-    reinterpret_cast<uint2*>(b)[s] = make_uint2(w[Q4 * 4], w[Q4 * 4 + 1]);
-    b += 2 * Spad;
-  }
-  if constexpr (R & 1) b[s] = w[NW - 1];
-}
-// host mirror of the plane layout
-inline size_t word_index(int NW, int Spad, int s, int k) {
-  const int Q4 = NW / 4, R = NW % 4;
-  if (k < Q4 * 4) return static_cast<size_t>(k / 4) * 4 * Spad + static_cast<size_t>(s) * 4 + (k % 4);
-  size_t b = static_cast<size_t>(Q4) * 4 * Spad;
-  if (R >= 2) {
-    if (k < Q4 * 4 + 2) return b + static_cast<size_t>(s) * 2 + (k - Q4 * 4);
-    b += 2 * static_cast<size_t>(Spad);
-  }
-  return b + s;
-}
-
-// New inputs of this tick.  kPacked: one [S][P] array; else one [S] array per
-// handle.  The host always passes valid pointers (a dummy when there is no new
-// input), so the loads are unconditional and issue with the others.
-template <class G, bool kPacked>
-__device__ __forceinline__ typename G::InRec gather_new_input(const KParams& p, unsigned s) {
-  using InRec = typename G::InRec;
-  constexpr int P = G::kPlayers, IB = G::kInputBytes;
-  if constexpr (kPacked && sizeof(InRec) == P * IB) {
-    return reinterpret_cast<const InRec*>(p.in_ptr[0])[s];
-  } else {
-    uint64_t v = 0;
-#pragma unroll
-    for (int q = 0; q < P; ++q) {
-      uint64_t x = 0;
-      if constexpr (kPacked) {
-        const uint8_t* b = reinterpret_cast<const uint8_t*>(p.in_ptr[0]) + (s * P + q) * IB;
-#pragma unroll
-        for (int i = 0; i < IB; ++i) x |= static_cast<uint64_t>(b[i]) << (8 * i);
-      } else if constexpr (IB == 4) {
-        x = reinterpret_cast<const uint32_t*>(p.in_ptr[q])[s];
-      } else {
-        x = reinterpret_cast<const uint8_t*>(p.in_ptr[q])[s];
-      }
-      v |= x << (8 * IB * q);
-    }
-    return static_cast<InRec>(v);
-  }
-}
-
-__host__ __device__ inline U128 to_u128(uint16_t c) { return U128{c, 0}; }
-__host__ __device__ inline U128 to_u128(uint64_t c) { return U128{c, 0}; }
-__host__ __device__ inline U128 to_u128(U128 c) { return c; }
-
-// snapshot slot of step k: (f0 + k) % W with f0 % W precomputed (k < 2W)
-__device__ __forceinline__ unsigned step_slot(const KParams& p, int k) {
-  int sl = p.slot0 + k;
-  sl = sl >= p.W ? sl - p.W : sl;
-  sl = sl >= p.W ? sl - p.W : sl;
-  return static_cast<unsigned>(sl);
-}
-
-// The fused tick.  Thread g serves lane (g % L) of session g / L; a session's
-// state slice stays in that lane's VGPRs for the whole tick.  Phase 1 issues
-// every load of the tick (frozen mask, new inputs, the loaded snapshot, the
-// inputs of every step, the first-seen checksums) before any store: on CDNA
-// vmcnt counts loads and stores in issue order, so a load issued after a
-// store would make its consumer wait for the store too.  Phase 2 performs the
-// input-queue writes, phase 3 runs the request stream: per step [SAVE:
-// checksum (lane-group DPP sum) + snapshot store + first-seen record/compare]
-// ADVANCE.
-template <class G, bool kPacked>
-__global__ void __launch_bounds__(256) tick_kernel(const KParams p) {
-  using InRec = typename G::InRec;
-  using CS = typename G::CS;
-  constexpr int NW = G::NWL;
-  constexpr unsigned L = G::kLanes;
-  const unsigned g = blockIdx.x * blockDim.x + threadIdx.x;
-  const unsigned s = g / L;
-  const int lane = static_cast<int>(g % L);
-  const bool lead = lane == 0;
-  if (s >= static_cast<unsigned>(p.S)) return;
-  {
-    const unsigned wave0 = __builtin_amdgcn_readfirstlane(s) & ~63u;
-    const unsigned long long fw = p.frozen[wave0 >> 6];
-    if ((fw >> (s & 63)) & 1ull) return;  // advance_frame keeps returning Err for this session
-  }
-  if (p.debug & 8u) return;  // launch floor (experiment)
-  const unsigned Spad = static_cast<unsigned>(p.Spad);
-  const unsigned Gpad = Spad * L;  // lane planes
-  InRec* __restrict__ ring = reinterpret_cast<InRec*>(p.ring);
-  CS* __restrict__ csa = reinterpret_cast<CS*>(p.cs);
-  const CS* __restrict__ fsa = reinterpret_cast<const CS*>(p.fs);
-  const unsigned slot_words = static_cast<unsigned>(NW) * Gpad;
-
-  // ---- phase 1: loads
-  const bool has_new = p.in_mode != 0 && p.user_slot >= 0;
-  const InRec newin = gather_new_input<G, kPacked>(p, s);
-  const InRec replv = ring[static_cast<unsigned>(p.repl_src) * Spad + s];
-  uint32_t w[NW];
-  if (p.load_slot >= 0)
-    load_words<NW>(p.snap + static_cast<unsigned>(p.load_slot) * slot_words, static_cast<int>(Gpad), static_cast<int>(g), w);
-  else
-    load_words<NW>(p.live, static_cast<int>(Gpad), static_cast<int>(g), w);
-
-  InRec in[kChunk];
-  CS fsv[kChunk];
-  auto prefetch = [&](int base) {
-#pragma unroll
-    for (int k = 0; k < kChunk; ++k) {
-      const int kk = base + k < p.n_steps ? base + k : base;  // clamp: always a valid address
-      in[k] = ring[static_cast<unsigned>((p.f0 + kk) & (kQueueLen - 1)) * Spad + s];
-      fsv[k] = fsa[step_slot(p, kk) * Spad + s];
-    }
-  };
-  prefetch(0);
-
-  // ---- phase 2: InputQueue::add_input for every handle (input_queue.rs:149-239):
-  // delay-fill replication, then the new inputs at frame current + delay.
-  if (lead) {
-    for (int r = 0; r < p.n_repl; ++r) ring[static_cast<unsigned>(p.repl_dst[r]) * Spad + s] = replv;
-    if (has_new) ring[static_cast<unsigned>(p.user_slot) * Spad + s] = newin;
-  }
-  auto patch = [&](int base) {  // prefetched slots that phase 2 just wrote
-#pragma unroll
-    for (int k = 0; k < kChunk; ++k) {
-      const int slot = (p.f0 + base + k) & (kQueueLen - 1);
-      for (int r = 0; r < p.n_repl; ++r)
-        if (slot == p.repl_dst[r]) in[k] = replv;
-      if (has_new && slot == p.user_slot) in[k] = newin;
-    }
-  };
-  patch(0);
-
-  // ---- phase 3: the request stream
-  CsCtx ctx{p.seed, s, p.nonce_base};
-  int32_t mismatch = kNullFrame;
-  for (int base = 0; base < p.n_steps; base += kChunk) {
-    if (base > 0) {
-      prefetch(base);
-      patch(base);
-    }
-#pragma unroll
-    for (int k = 0; k < kChunk; ++k) {
-      const int step = base + k;
-      if (step >= p.n_steps) break;
-      const int32_t f = p.f0 + step;
-      const uint32_t mode = (p.save_modes[step >> 4] >> ((step & 15) * 2)) & 3u;
-      if (mode != SAVE_NONE) {  // SaveGameState{cell, f}: checksum, cell.save
-        ctx.nonce = p.nonce_base + static_cast<uint32_t>(step);
-        const CS c = (p.debug & 4u) ? CS{} : G::checksum(w, f, lane, ctx);
-        const unsigned slot = step_slot(p, step);
-        if (!(p.debug & 2u))
-          store_words<NW>(p.snap + slot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), w);
-        if (lead) csa[slot * Spad + s] = c;
-        if (mode == SAVE_RECORD) {
-          if (lead) reinterpret_cast<CS*>(p.fs)[slot * Spad + s] = c;
-        } else if (mode == SAVE_COMPARE) {
-          if (c != fsv[k]) mismatch = f;  // newest mismatching frame wins
-        }
-      }
-      if (p.debug & 1u)
-        w[0] += in[k];
-      else
-        G::advance(w, in[k], lane, p.disc_mask, &p.counters[1]);  // AdvanceFrame{inputs}
-      if (step == p.periodic_step) {
-        ctx.nonce = p.nonce_base + 128u + static_cast<uint32_t>(step);
-        const CS c = G::checksum(w, f + 1, lane, ctx);
-        if (lead) reinterpret_cast<CS*>(p.periodic_cs)[s] = c;
-      }
-    }
-  }
-  if (p.display) {  // Game::last_checksum after the final AdvanceFrame (ex_game.rs:104-108)
-    ctx.nonce = p.nonce_base + 255u;
-    const CS c = G::checksum(w, p.f0 + p.n_steps, lane, ctx);
-    if (lead) reinterpret_cast<CS*>(p.last_cs)[s] = c;
-  }
-  if (p.live_out || mismatch != kNullFrame) store_words<NW>(p.live, static_cast<int>(Gpad), static_cast<int>(g), w);
-  if (mismatch != kNullFrame && lead) {
-    p.err[s] = mismatch;
-    p.live_frame[s] = p.f0 + p.n_steps;  // the session stops at the end of this tick
-    atomicOr(&p.frozen[s >> 6], 1ull << (s & 63));
-    atomicAdd(&p.counters[0], 1u);
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Fused steady-state SyncTest ticks (rb_run_ticks).  For current frame c > cd
-// the reference's stream is always (sync_test_session.rs:89-132, 178-203)
-//   Load(c-cd), Adv, [Save(f) Adv] for f = c-cd+1 .. c-1, Save(c), Adv
-// so T consecutive such ticks run in ONE launch with the shape known at
-// compile time (CD = check distance): no per-tick launch, no per-step control
-// flow, and each wave keeps its sessions across ticks (the slot it loads was
-// written by the same lanes one tick earlier, so it is L2-hot).  Every
-// request still executes against memory exactly as in tick_kernel: the
-// snapshot is loaded from its cell, every save stores the cell, the inputs
-// come from the input queue ring.  The host bookkeeping runs per tick as
-// usual; only ticks whose lowered program has exactly this shape are fused.
-struct RunParams {
-  uint32_t* snap;
-  void* cs;
-  void* fs;
-  void* ring;
-  void* last_cs;
-  void* periodic_cs;
-  uint32_t* live;
-  int32_t* err;
-  int32_t* live_frame;
-  unsigned long long* frozen;
-  uint32_t* counters;
-  const uint8_t* in_base;  // tick t, player q: in_base + t*in_stride + q*S*kInputBytes
-  int64_t in_stride;
-  int32_t S, Spad, W, delay;
-  int32_t c0, T;            // current frame of the first fused tick, tick count
-  uint32_t tick0;           // engine tick index of the first fused tick (nonce)
-  int32_t live_out_last;    // store the live state after the last tick
-  uint64_t seed;
-};
-
-template <class G, int CD>
-__global__ void __launch_bounds__(256) steady_kernel(const RunParams p) {
-  static_assert(CD >= 1, "steady shape needs a rollback");
-  using InRec = typename G::InRec;
-  using CS = typename G::CS;
-  constexpr int NW = G::NWL;
-  constexpr unsigned L = G::kLanes;
-  constexpr int P = G::kPlayers, IB = G::kInputBytes;
-  const unsigned g = blockIdx.x * blockDim.x + threadIdx.x;
-  const unsigned s = g / L;
-  const int lane = static_cast<int>(g % L);
-  const bool lead = lane == 0;
-  if (s >= static_cast<unsigned>(p.S)) return;
-  {
-    const unsigned wave0 = __builtin_amdgcn_readfirstlane(s) & ~63u;
-    if ((p.frozen[wave0 >> 6] >> (s & 63)) & 1ull) return;
-  }
-  const unsigned Spad = static_cast<unsigned>(p.Spad), Gpad = Spad * L;
-  const unsigned slot_words = static_cast<unsigned>(NW) * Gpad;
-  InRec* __restrict__ ring = reinterpret_cast<InRec*>(p.ring);
-  CS* __restrict__ csa = reinterpret_cast<CS*>(p.cs);
-  CS* __restrict__ fsa = reinterpret_cast<CS*>(p.fs);
-  const int W = p.W;
-  auto slot_of = [W](int f) { return static_cast<unsigned>(f % W); };
-
-  for (int t = 0; t < p.T; ++t) {
-    const int c = p.c0 + t;
-    const int f0 = c - CD;
-    // ---- loads of the tick
-    const uint8_t* tin = p.in_base + static_cast<int64_t>(t) * p.in_stride;
-    uint64_t nv = 0;
-#pragma unroll
-    for (int q = 0; q < P; ++q) {
-      uint64_t x;
-      if constexpr (IB == 4)
-        x = reinterpret_cast<const uint32_t*>(tin + static_cast<size_t>(q) * p.S * IB)[s];
-      else
-        x = tin[static_cast<size_t>(q) * p.S + s];
-      nv |= x << (8 * IB * q);
-    }
-    const InRec newin = static_cast<InRec>(nv);
-    uint32_t w[NW];
-    load_words<NW>(p.snap + slot_of(f0) * slot_words, static_cast<int>(Gpad), static_cast<int>(g), w);
-    InRec in[CD + 1];
-#pragma unroll
-    for (int k = 0; k <= CD; ++k) in[k] = ring[static_cast<unsigned>((f0 + k) & (kQueueLen - 1)) * Spad + s];
-    CS fsv[CD > 1 ? CD - 1 : 1];
-#pragma unroll
-    for (int k = 1; k < CD; ++k) fsv[k - 1] = fsa[slot_of(f0 + k) * Spad + s];
-    // ---- InputQueue::add_input for every handle: the new inputs at c + delay
-    const unsigned uslot = static_cast<unsigned>((c + p.delay) & (kQueueLen - 1));
-    if (lead) ring[uslot * Spad + s] = newin;
-    if (p.delay == 0) in[CD] = newin;
-    // ---- the request stream
-    const uint32_t nonce = ((p.tick0 + static_cast<uint32_t>(t)) & 0xffffffu) << 8;
-    CsCtx ctx{p.seed, s, nonce};
-    int32_t mismatch = kNullFrame;
-#pragma unroll
-    for (int k = 0; k <= CD; ++k) {
-      const int f = f0 + k;
-      if (k > 0) {  // SaveGameState{cell, f}
-        ctx.nonce = nonce + static_cast<uint32_t>(k);
-        const CS cval = G::checksum(w, f, lane, ctx);
-        const unsigned slot = slot_of(f);
-        store_words<NW>(p.snap + slot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), w);
-        if (lead) csa[slot * Spad + s] = cval;
-        if (k == CD) {
-          if (lead) fsa[slot * Spad + s] = cval;  // first save of frame c: first-seen
-        } else if (cval != fsv[k - 1]) {
-          mismatch = f;  // newest mismatching frame wins
-        }
-      }
-      G::advance(w, in[k], lane, 0u, &p.counters[1]);  // AdvanceFrame{inputs}
-      if ((f + 1) % 100 == 0) {  // ex_game periodic_checksum (frame % CHECKSUM_PERIOD == 0)
-        ctx.nonce = nonce + 128u + static_cast<uint32_t>(k);
-        const CS cval = G::checksum(w, f + 1, lane, ctx);
-        if (G::kDisplay && lead) reinterpret_cast<CS*>(p.periodic_cs)[s] = cval;
-      }
-    }
-    if constexpr (G::kDisplay) {  // Game::last_checksum after the final AdvanceFrame
-      ctx.nonce = nonce + 255u;
-      const CS cval = G::checksum(w, c + 1, lane, ctx);
-      if (lead) reinterpret_cast<CS*>(p.last_cs)[s] = cval;
-    }
-    if (mismatch != kNullFrame) {
-      store_words<NW>(p.live, static_cast<int>(Gpad), static_cast<int>(g), w);
-      if (lead) {
-        p.err[s] = mismatch;
-        p.live_frame[s] = c + 1;
-        atomicOr(&p.frozen[s >> 6], 1ull << (s & 63));
-        atomicAdd(&p.counters[0], 1u);
-      }
-      return;  // advance_frame returns Err for this session from the next tick on
-    }
-    if (t == p.T - 1 && p.live_out_last) store_words<NW>(p.live, static_cast<int>(Gpad), static_cast<int>(g), w);
-  }
-}
-
-template <class G>
-__global__ void report_kernel(const typename G::CS* __restrict__ cs, const int32_t* __restrict__ err, int S,
-                              int32_t frame, rb_checksum_report* __restrict__ out) {
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= S) return;
-  const U128 c = to_u128(cs[s]);
-  rb_checksum_report r;
-  r.checksum_lo = c.lo;
-  r.checksum_hi = c.hi;
-  r.frame = frame;
-  r.mismatch_frame = err[s];
-  out[s] = r;
-}
-
 __global__ void sincos_kernel(const float* __restrict__ x, float* __restrict__ so, float* __restrict__ co, int64_t n,
                               uint32_t* unexpected) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -428,108 +41,13 @@ __global__ void sincos_kernel(const float* __restrict__ x, float* __restrict__ s
   co[i] = r.c;
 }
 
-}  // namespace rb
-
-// ============================================================================
-// host side
-// ============================================================================
-namespace rb {
-struct GameOps {
-  virtual ~GameOps() = default;
-  int nw = 0, lanes = 1, players = 0, input_bytes = 0, inrec_bytes = 0, cs_bytes = 0, image_bytes = 0, canon_words = 0;
-  bool display = false;
-  virtual void word_loc(int k, int* lane, int* word) const = 0;
-  virtual void init_words(uint32_t* w) const = 0;
-  virtual void image(const uint32_t* w, int32_t frame, uint8_t* out) const = 0;
-  virtual U128 cs_at(const void* arr, size_t i) const = 0;
-  virtual hipError_t launch_tick(const KParams& p, int block, hipStream_t st) const = 0;
-  // fused steady-state ticks; hipErrorNotSupported when CD has no instantiation
-  virtual hipError_t launch_steady(const RunParams& p, int cd, int block, hipStream_t st) const = 0;
-  bool launch_steady_supported(int cd) const { return cd >= 1 && cd <= 8; }
-  virtual hipError_t launch_report(const void* cs, const int32_t* err, int S, int32_t frame, void* out,
-                                   hipStream_t st) const = 0;
-};
-
-template <class G>
-struct GameOpsT final : GameOps {
-  GameOpsT() {
-    nw = G::NWL;
-    lanes = G::kLanes;
-    canon_words = G::kCanonWords;
-    players = G::kPlayers;
-    input_bytes = G::kInputBytes;
-    inrec_bytes = sizeof(typename G::InRec);
-    cs_bytes = sizeof(typename G::CS);
-    image_bytes = G::kImageBytes;
-    display = G::kDisplay;
-  }
-  void word_loc(int k, int* lane, int* word) const override { G::word_loc(k, lane, word); }
-  void init_words(uint32_t* w) const override { G::init(w); }
-  void image(const uint32_t* w, int32_t frame, uint8_t* out) const override { G::image(w, frame, out); }
-  U128 cs_at(const void* arr, size_t i) const override {
-    return to_u128(reinterpret_cast<const typename G::CS*>(arr)[i]);
-  }
-  hipError_t launch_tick(const KParams& p, int block, hipStream_t st) const override {
-    const int grid = (p.Spad * G::kLanes + block - 1) / block;
-    if (p.in_mode == 2)
-      hipLaunchKernelGGL((tick_kernel<G, true>), dim3(grid), dim3(block), 0, st, p);
-    else
-      hipLaunchKernelGGL((tick_kernel<G, false>), dim3(grid), dim3(block), 0, st, p);
-    return hipGetLastError();
-  }
-  template <int CD>
-  static hipError_t steady_cd(const RunParams& p, int block, hipStream_t st) {
-    const int grid = (p.Spad * G::kLanes + block - 1) / block;
-    hipLaunchKernelGGL((steady_kernel<G, CD>), dim3(grid), dim3(block), 0, st, p);
-    return hipGetLastError();
-  }
-  hipError_t launch_steady(const RunParams& p, int cd, int block, hipStream_t st) const override {
-    switch (cd) {
-      case 1: return steady_cd<1>(p, block, st);
-      case 2: return steady_cd<2>(p, block, st);
-      case 3: return steady_cd<3>(p, block, st);
-      case 4: return steady_cd<4>(p, block, st);
-      case 5: return steady_cd<5>(p, block, st);
-      case 6: return steady_cd<6>(p, block, st);
-      case 7: return steady_cd<7>(p, block, st);
-      case 8: return steady_cd<8>(p, block, st);
-      default: return hipErrorNotSupported;
-    }
-  }
-  hipError_t launch_report(const void* cs, const int32_t* err, int S, int32_t frame, void* out,
-                           hipStream_t st) const override {
-    hipLaunchKernelGGL(report_kernel<G>, dim3((S + 255) / 256), dim3(256), 0, st,
-                       reinterpret_cast<const typename G::CS*>(cs), err, S, frame,
-                       reinterpret_cast<rb_checksum_report*>(out));
-    return hipGetLastError();
-  }
-};
-
-template <bool kSplit>
-inline std::unique_ptr<GameOps> make_ex_game(int players) {
-  switch (players) {
-    case 1: return std::make_unique<GameOpsT<ExGame<1, kSplit>>>();
-    case 2: return std::make_unique<GameOpsT<ExGame<2, kSplit>>>();
-    case 3: return std::make_unique<GameOpsT<ExGame<3, kSplit>>>();
-    case 4: return std::make_unique<GameOpsT<ExGame<4, kSplit>>>();
-    default: return nullptr;
-  }
-}
-
 inline std::unique_ptr<GameOps> make_game(int game, int players, bool lane_per_session) {
   switch (game) {
-    case RB_GAME_EX_GAME: return lane_per_session ? make_ex_game<false>(players) : make_ex_game<true>(players);
-    case RB_GAME_STUB: return players == 2 ? std::make_unique<GameOpsT<StubGame>>() : nullptr;
-    case RB_GAME_STUB_ENUM: return players == 2 ? std::make_unique<GameOpsT<StubEnumGame>>() : nullptr;
-    case RB_GAME_STUB_RANDOM_CS: return players == 2 ? std::make_unique<GameOpsT<StubRandomCsGame>>() : nullptr;
-    case RB_GAME_BRAWLER:
-      switch (players) {
-        case 1: return std::make_unique<GameOpsT<Brawler<1>>>();
-        case 2: return std::make_unique<GameOpsT<Brawler<2>>>();
-        case 3: return std::make_unique<GameOpsT<Brawler<3>>>();
-        case 4: return std::make_unique<GameOpsT<Brawler<4>>>();
-        default: return nullptr;
-      }
+    case RB_GAME_EX_GAME: return make_exgame_ops(players, lane_per_session);
+    case RB_GAME_BRAWLER: return make_brawler_ops(players);
+    case RB_GAME_STUB:
+    case RB_GAME_STUB_ENUM:
+    case RB_GAME_STUB_RANDOM_CS: return make_stub_ops(game, players);
     default: return nullptr;
   }
 }
@@ -959,6 +477,7 @@ rb_status launch_steady_run(rb_batch* b, const uint8_t* tick_inputs, int64_t str
   r.tick0 = tick0;
   r.live_out_last = 0;
   r.seed = b->cfg.seed;
+  r.debug = b->cfg.reserved[0];
   const bool timed = b->prof;
   if (timed) {
     if (b->prof_used == b->prof_ev.size()) {

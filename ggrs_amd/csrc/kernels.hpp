@@ -1,0 +1,567 @@
+// ggrs_amd/csrc/kernels.hpp — device kernels of the batched rollback engine and the
+// per-game launcher (GameOpsT).  Included by every ops_*.hip translation unit, each
+// of which instantiates the kernels of its own games (so the device code of the
+// games compiles in parallel), and by engine.hip for the shared types.
+//
+// One rb_batch = S independent SyncTestSessions in lock-step.  Per tick the
+// host mirror (planner.hpp) produces the reference's request stream and lowers
+// it to a TickProgram; ONE kernel launch then executes that stream for every
+// session: lane s owns session s, its state stays in VGPRs from the
+// LoadGameState through every SaveGameState/AdvanceFrame of the tick, and
+// HBM sees each snapshot written once (coalesced SoA planes) and the loaded
+// slot read once.
+//
+// Device layout (Spad = S rounded up to 64; all planes contiguous over sessions):
+//   snap  [W slots][NW words as planes of u32x4 / u32x2 / u32][Spad]   snapshot ring, slot = frame % W
+//   cs    [W][Spad] CS        checksum stored by each SaveGameState (GameStateCell::checksum)
+//   fs    [W][Spad] CS        first-seen checksum of the frame (SyncTestSession::checksum_history)
+//   ring  [128][Spad] InRec   confirmed inputs, slot = frame % 128 (InputQueue::inputs)
+//   live  [NW planes][Spad]   live game state between ticks when no LoadGameState follows
+//   err   [Spad] i32          MismatchedChecksum{frame}, NULL_FRAME when healthy
+//   frozen[Spad/64] u64       sessions whose advance_frame returns Err (they no longer advance)
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <memory>
+
+#include "../../include/ggrs_amd.h"
+#include "games.hpp"
+#include "planner.hpp"
+
+namespace rb {
+
+constexpr int kChunk = 8;  // inputs prefetched per chunk of AdvanceFrames
+constexpr int kMaxRepl = 8;
+
+struct KParams {
+  uint32_t* snap;
+  uint32_t* live;
+  void* cs;
+  void* fs;
+  void* ring;
+  void* last_cs;
+  void* periodic_cs;
+  int32_t* err;
+  int32_t* live_frame;
+  unsigned long long* frozen;
+  uint32_t* counters;  // [0] sessions failed, [1] unexpected-path count
+  const void* in_ptr[4];
+  int32_t in_mode;  // 0: no new input, 1: one array per player, 2: packed [S][P]
+  int32_t S, Spad, W;
+  int32_t user_slot, n_repl, repl_src;
+  int32_t repl_dst[kMaxRepl];
+  int32_t load_slot;  // -1: start from the live state
+  int32_t f0, n_steps;
+  uint32_t save_modes[kMaxSteps / 16];  // 2 bits per step
+  int32_t slot0;                        // f0 % W (snapshot slot of step 0)
+  int32_t live_out, periodic_step, display;
+  uint32_t disc_mask;
+  uint64_t seed;
+  uint32_t nonce_base;
+  uint32_t debug;  // experiment knobs (rb_config.reserved[0]); 0 in every real run
+};
+
+// ---- SoA planes: word k of session s inside a block of NW planes -------------
+template <int NW>
+__device__ __forceinline__ void load_words(const uint32_t* __restrict__ base, int Spad, int s, uint32_t (&w)[NW]) {
+  constexpr int Q4 = NW / 4, R = NW % 4;
+#pragma unroll
+  for (int j = 0; j < Q4; ++j) {
+    const uint4 v = reinterpret_cast<const uint4*>(base + j * 4 * Spad)[s];
+    w[4 * j + 0] = v.x;
+    w[4 * j + 1] = v.y;
+    w[4 * j + 2] = v.z;
+    w[4 * j + 3] = v.w;
+  }
+  const uint32_t* b = base + Q4 * 4 * Spad;
+  if constexpr (R >= 2) {
+    const uint2 v = reinterpret_cast<const uint2*>(b)[s];
+    w[Q4 * 4 + 0] = v.x;
+    w[Q4 * 4 + 1] = v.y;
+    b += 2 * Spad;
+  }
+  if constexpr (R & 1) w[NW - 1] = b[s];
+}
+template <int NW>
+__device__ __forceinline__ void store_words(uint32_t* __restrict__ base, int Spad, int s, const uint32_t (&w)[NW]) {
+  constexpr int Q4 = NW / 4, R = NW % 4;
+#pragma unroll
+  for (int j = 0; j < Q4; ++j)
+    reinterpret_cast<uint4*>(base + j * 4 * Spad)[s] = make_uint4(w[4 * j], w[4 * j + 1], w[4 * j + 2], w[4 * j + 3]);
+  uint32_t* b = base + Q4 * 4 * Spad;
+  if constexpr (R >= 2) {
+    reinterpret_cast<uint2*>(b)[s] = make_uint2(w[Q4 * 4], w[Q4 * 4 + 1]);
+    b += 2 * Spad;
+  }
+  if constexpr (R & 1) b[s] = w[NW - 1];
+}
+// host mirror of the plane layout
+inline size_t word_index(int NW, int Spad, int s, int k) {
+  const int Q4 = NW / 4, R = NW % 4;
+  if (k < Q4 * 4) return static_cast<size_t>(k / 4) * 4 * Spad + static_cast<size_t>(s) * 4 + (k % 4);
+  size_t b = static_cast<size_t>(Q4) * 4 * Spad;
+  if (R >= 2) {
+    if (k < Q4 * 4 + 2) return b + static_cast<size_t>(s) * 2 + (k - Q4 * 4);
+    b += 2 * static_cast<size_t>(Spad);
+  }
+  return b + s;
+}
+
+// New inputs of this tick.  kPacked: one [S][P] array; else one [S] array per
+// handle.  The host always passes valid pointers (a dummy when there is no new
+// input), so the loads are unconditional and issue with the others.
+template <class G, bool kPacked>
+__device__ __forceinline__ typename G::InRec gather_new_input(const KParams& p, unsigned s) {
+  using InRec = typename G::InRec;
+  constexpr int P = G::kPlayers, IB = G::kInputBytes;
+  if constexpr (kPacked && sizeof(InRec) == P * IB) {
+    return reinterpret_cast<const InRec*>(p.in_ptr[0])[s];
+  } else {
+    uint64_t v = 0;
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+      uint64_t x = 0;
+      if constexpr (kPacked) {
+        const uint8_t* b = reinterpret_cast<const uint8_t*>(p.in_ptr[0]) + (s * P + q) * IB;
+#pragma unroll
+        for (int i = 0; i < IB; ++i) x |= static_cast<uint64_t>(b[i]) << (8 * i);
+      } else if constexpr (IB == 4) {
+        x = reinterpret_cast<const uint32_t*>(p.in_ptr[q])[s];
+      } else {
+        x = reinterpret_cast<const uint8_t*>(p.in_ptr[q])[s];
+      }
+      v |= x << (8 * IB * q);
+    }
+    return static_cast<InRec>(v);
+  }
+}
+
+__host__ __device__ inline U128 to_u128(uint16_t c) { return U128{c, 0}; }
+__host__ __device__ inline U128 to_u128(uint64_t c) { return U128{c, 0}; }
+__host__ __device__ inline U128 to_u128(U128 c) { return c; }
+
+// snapshot slot of step k: (f0 + k) % W with f0 % W precomputed (k < 2W)
+__device__ __forceinline__ unsigned step_slot(const KParams& p, int k) {
+  int sl = p.slot0 + k;
+  sl = sl >= p.W ? sl - p.W : sl;
+  sl = sl >= p.W ? sl - p.W : sl;
+  return static_cast<unsigned>(sl);
+}
+
+// The fused tick.  Thread g serves lane (g % L) of session g / L; a session's
+// state slice stays in that lane's VGPRs for the whole tick.  Phase 1 issues
+// every load of the tick (frozen mask, new inputs, the loaded snapshot, the
+// inputs of every step, the first-seen checksums) before any store: on CDNA
+// vmcnt counts loads and stores in issue order, so a load issued after a
+// store would make its consumer wait for the store too.  Phase 2 performs the
+// input-queue writes, phase 3 runs the request stream: per step [SAVE:
+// checksum (lane-group DPP sum) + snapshot store + first-seen record/compare]
+// ADVANCE.
+template <class G, bool kPacked>
+__global__ void __launch_bounds__(256) tick_kernel(const KParams p) {
+  using InRec = typename G::InRec;
+  using CS = typename G::CS;
+  constexpr int NW = G::NWL;
+  constexpr unsigned L = G::kLanes;
+  const unsigned g = blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned s = g / L;
+  const int lane = static_cast<int>(g % L);
+  const bool lead = lane == 0;
+  if (s >= static_cast<unsigned>(p.S)) return;
+  {
+    const unsigned wave0 = __builtin_amdgcn_readfirstlane(s) & ~63u;
+    const unsigned long long fw = p.frozen[wave0 >> 6];
+    if ((fw >> (s & 63)) & 1ull) return;  // advance_frame keeps returning Err for this session
+  }
+  if (p.debug & 8u) return;  // launch floor (experiment)
+  const unsigned Spad = static_cast<unsigned>(p.Spad);
+  const unsigned Gpad = Spad * L;  // lane planes
+  InRec* __restrict__ ring = reinterpret_cast<InRec*>(p.ring);
+  CS* __restrict__ csa = reinterpret_cast<CS*>(p.cs);
+  const CS* __restrict__ fsa = reinterpret_cast<const CS*>(p.fs);
+  const unsigned slot_words = static_cast<unsigned>(NW) * Gpad;
+
+  // ---- phase 1: loads
+  const bool has_new = p.in_mode != 0 && p.user_slot >= 0;
+  const InRec newin = gather_new_input<G, kPacked>(p, s);
+  const InRec replv = ring[static_cast<unsigned>(p.repl_src) * Spad + s];
+  uint32_t w[NW];
+  if (p.load_slot >= 0)
+    load_words<NW>(p.snap + static_cast<unsigned>(p.load_slot) * slot_words, static_cast<int>(Gpad), static_cast<int>(g), w);
+  else
+    load_words<NW>(p.live, static_cast<int>(Gpad), static_cast<int>(g), w);
+
+  InRec in[kChunk];
+  CS fsv[kChunk];
+  auto prefetch = [&](int base) {
+#pragma unroll
+    for (int k = 0; k < kChunk; ++k) {
+      const int kk = base + k < p.n_steps ? base + k : base;  // clamp: always a valid address
+      in[k] = ring[static_cast<unsigned>((p.f0 + kk) & (kQueueLen - 1)) * Spad + s];
+      fsv[k] = fsa[step_slot(p, kk) * Spad + s];
+    }
+  };
+  prefetch(0);
+
+  // ---- phase 2: InputQueue::add_input for every handle (input_queue.rs:149-239):
+  // delay-fill replication, then the new inputs at frame current + delay.
+  if (lead) {
+    for (int r = 0; r < p.n_repl; ++r) ring[static_cast<unsigned>(p.repl_dst[r]) * Spad + s] = replv;
+    if (has_new) ring[static_cast<unsigned>(p.user_slot) * Spad + s] = newin;
+  }
+  auto patch = [&](int base) {  // prefetched slots that phase 2 just wrote
+#pragma unroll
+    for (int k = 0; k < kChunk; ++k) {
+      const int slot = (p.f0 + base + k) & (kQueueLen - 1);
+      for (int r = 0; r < p.n_repl; ++r)
+        if (slot == p.repl_dst[r]) in[k] = replv;
+      if (has_new && slot == p.user_slot) in[k] = newin;
+    }
+  };
+  patch(0);
+
+  // ---- phase 3: the request stream
+  CsCtx ctx{p.seed, s, p.nonce_base};
+  int32_t mismatch = kNullFrame;
+  for (int base = 0; base < p.n_steps; base += kChunk) {
+    if (base > 0) {
+      prefetch(base);
+      patch(base);
+    }
+#pragma unroll
+    for (int k = 0; k < kChunk; ++k) {
+      const int step = base + k;
+      if (step >= p.n_steps) break;
+      const int32_t f = p.f0 + step;
+      const uint32_t mode = (p.save_modes[step >> 4] >> ((step & 15) * 2)) & 3u;
+      if (mode != SAVE_NONE) {  // SaveGameState{cell, f}: checksum, cell.save
+        ctx.nonce = p.nonce_base + static_cast<uint32_t>(step);
+        const CS c = (p.debug & 4u) ? CS{} : G::checksum(w, f, lane, ctx);
+        const unsigned slot = step_slot(p, step);
+        if (!(p.debug & 2u))
+          store_words<NW>(p.snap + slot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), w);
+        if (lead) csa[slot * Spad + s] = c;
+        if (mode == SAVE_RECORD) {
+          if (lead) reinterpret_cast<CS*>(p.fs)[slot * Spad + s] = c;
+        } else if (mode == SAVE_COMPARE) {
+          if (c != fsv[k]) mismatch = f;  // newest mismatching frame wins
+        }
+      }
+      if (p.debug & 1u)
+        w[0] += in[k];
+      else
+        G::advance(w, in[k], lane, p.disc_mask, &p.counters[1]);  // AdvanceFrame{inputs}
+      if (step == p.periodic_step) {
+        ctx.nonce = p.nonce_base + 128u + static_cast<uint32_t>(step);
+        const CS c = G::checksum(w, f + 1, lane, ctx);
+        if (lead) reinterpret_cast<CS*>(p.periodic_cs)[s] = c;
+      }
+    }
+  }
+  if (p.display) {  // Game::last_checksum after the final AdvanceFrame (ex_game.rs:104-108)
+    ctx.nonce = p.nonce_base + 255u;
+    const CS c = G::checksum(w, p.f0 + p.n_steps, lane, ctx);
+    if (lead) reinterpret_cast<CS*>(p.last_cs)[s] = c;
+  }
+  if (p.live_out || mismatch != kNullFrame) store_words<NW>(p.live, static_cast<int>(Gpad), static_cast<int>(g), w);
+  if (mismatch != kNullFrame && lead) {
+    p.err[s] = mismatch;
+    p.live_frame[s] = p.f0 + p.n_steps;  // the session stops at the end of this tick
+    atomicOr(&p.frozen[s >> 6], 1ull << (s & 63));
+    atomicAdd(&p.counters[0], 1u);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Fused steady-state SyncTest ticks (rb_run_ticks).  For current frame c > cd
+// the reference's stream is always (sync_test_session.rs:89-132, 178-203)
+//   Load(c-cd), Adv, [Save(f) Adv] for f = c-cd+1 .. c-1, Save(c), Adv
+// so T consecutive such ticks run in ONE launch with the shape known at
+// compile time (CD = check distance): no per-tick launch, no per-step control
+// flow, and each wave keeps its sessions across ticks.  Every request still
+// executes against memory exactly as in tick_kernel: every save stores the
+// cell, its checksum and (frame c) the first-seen record, the new inputs are
+// written to the input-queue ring, and each tick's LoadGameState reads its
+// cell back from memory.  What a tick needs is fetched a tick ahead, so no
+// load sits on the critical path of the 8 serial AdvanceFrames:
+//  * the next tick loads cell c+1-CD, which this tick saves at its step 1:
+//    the load is issued right after that store (same lane and address, so
+//    program order returns the stored bytes) and consumed CD-1 steps later;
+//  * inputs and first-seen checksums already known to the launch slide
+//    through register windows; the one new input per tick comes from the
+//    read-only per-tick input buffer, never from a ring entry this launch
+//    wrote.
+// The host bookkeeping runs per tick as usual; only ticks whose lowered
+// program has exactly this shape are fused.
+struct RunParams {
+  uint32_t* snap;
+  void* cs;
+  void* fs;
+  void* ring;
+  void* last_cs;
+  void* periodic_cs;
+  uint32_t* live;
+  int32_t* err;
+  int32_t* live_frame;
+  unsigned long long* frozen;
+  uint32_t* counters;
+  const uint8_t* in_base;  // tick t, player q: in_base + t*in_stride + q*S*kInputBytes
+  int64_t in_stride;
+  int32_t S, Spad, W, delay;
+  int32_t c0, T;            // current frame of the first fused tick, tick count
+  uint32_t tick0;           // engine tick index of the first fused tick (nonce)
+  int32_t live_out_last;    // store the live state after the last tick
+  uint64_t seed;
+  uint32_t debug;           // experiment knobs (rb_config.reserved[0]); 0 in every real run
+};
+
+// An empty asm that reads v: the compiler must complete the load that
+// produced v before this point (an s_waitcnt counted within the iteration).
+__device__ __forceinline__ void settle(uint32_t v) { asm volatile("" ::"v"(v)); }
+
+template <class G, int CD>
+__global__ void __launch_bounds__(256) steady_kernel(const RunParams p) {
+  static_assert(CD >= 1, "steady shape needs a rollback");
+  using InRec = typename G::InRec;
+  using CS = typename G::CS;
+  constexpr int NW = G::NWL;
+  constexpr unsigned L = G::kLanes;
+  constexpr int P = G::kPlayers, IB = G::kInputBytes;
+  constexpr int NF = CD > 1 ? CD - 1 : 1;  // first-seen window: frames f0+1 .. f0+CD-1
+  const unsigned g = blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned s = g / L;
+  const int lane = static_cast<int>(g % L);
+  const bool lead = lane == 0;
+  if (s >= static_cast<unsigned>(p.S)) return;
+  {
+    const unsigned wave0 = __builtin_amdgcn_readfirstlane(s) & ~63u;
+    if ((p.frozen[wave0 >> 6] >> (s & 63)) & 1ull) return;
+  }
+  const unsigned Spad = static_cast<unsigned>(p.Spad), Gpad = Spad * L;
+  const unsigned slot_words = static_cast<unsigned>(NW) * Gpad;
+  InRec* __restrict__ ring = reinterpret_cast<InRec*>(p.ring);
+  CS* __restrict__ csa = reinterpret_cast<CS*>(p.cs);
+  CS* __restrict__ fsa = reinterpret_cast<CS*>(p.fs);
+  const int W = p.W;
+  auto slot_of = [W](int f) { return static_cast<unsigned>(f % W); };
+  // The new inputs of launch tick tt (the read-only per-tick input buffer).
+  auto new_input = [&](int tt) -> InRec {
+    const uint8_t* tin = p.in_base + static_cast<int64_t>(tt) * p.in_stride;
+    uint64_t v = 0;
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+      uint64_t x;
+      if constexpr (IB == 4)
+        x = reinterpret_cast<const uint32_t*>(tin + static_cast<size_t>(q) * p.S * IB)[s];
+      else
+        x = tin[static_cast<size_t>(q) * p.S + s];
+      v |= x << (8 * IB * q);
+    }
+    return static_cast<InRec>(v);
+  };
+  // InputQueue::input(frame) for a confirmed frame: the input added at tick
+  // frame - delay.  Inside this launch that is that tick's new input (read
+  // from the input buffer, never from a ring entry this launch wrote); older
+  // frames come from the ring as written before the launch.  Wave-uniform.
+  // Both loads are issued unconditionally and selected: a branch around a
+  // load makes the compiler wait for it (and every older store) at the join.
+  auto input_of_frame = [&](int fr) -> InRec {
+    const int tt = fr - p.delay - p.c0;
+    const InRec a = new_input(tt >= 0 ? tt : 0);
+    const InRec b = ring[static_cast<unsigned>(fr & (kQueueLen - 1)) * Spad + s];
+    return tt >= 0 ? a : b;
+  };
+
+  // Prologue: the first tick's snapshot, input window and first-seen window.
+  // Later ticks get them from registers (inputs, first-seen values this
+  // launch recorded) or from a load issued one tick ahead (the snapshot).
+  int f0 = p.c0 - CD;
+  uint32_t w[NW];
+  load_words<NW>(p.snap + slot_of(f0) * slot_words, static_cast<int>(Gpad), static_cast<int>(g), w);
+  InRec win[CD + 1];  // inputs of frames f0 .. f0+CD
+#pragma unroll
+  for (int k = 0; k <= CD; ++k) win[k] = input_of_frame(f0 + k);
+  CS fsw[NF];  // SyncTest first-seen checksums of frames f0+1 .. f0+CD-1
+#pragma unroll
+  for (int k = 1; k < CD; ++k) fsw[k - 1] = fsa[slot_of(f0 + k) * Spad + s];
+
+  // A load whose value is used after a store waits for that store too (vmcnt
+  // retires loads and stores in issue order), so every input load is issued
+  // one tick before it is used, ahead of that tick's stores.
+  InRec newin = new_input(0);
+  for (int t = 0; t < p.T; ++t) {
+    const int c = p.c0 + t;
+    const bool more = t + 1 < p.T;
+    // ---- the next tick's inputs (read-only sources), before this tick's stores
+    const InRec newin_next = new_input(more ? t + 1 : t);
+    const InRec next_last = input_of_frame(more ? c + 1 : c);  // frame f0+CD+1 of the next tick
+    // ---- InputQueue::add_input for every handle: the new inputs at c + delay
+    if (lead) ring[static_cast<unsigned>((c + p.delay) & (kQueueLen - 1)) * Spad + s] = newin;
+    // ---- the request stream
+    const uint32_t nonce = ((p.tick0 + static_cast<uint32_t>(t)) & 0xffffffu) << 8;
+    CsCtx ctx{p.seed, s, nonce};
+    int32_t mismatch = kNullFrame;
+    CS recorded{};
+    uint32_t wn[NW];  // next tick's LoadGameState(c+1-CD), loaded right after this tick saves it
+#pragma unroll
+    for (int k = 0; k <= CD; ++k) {
+      const int f = f0 + k;
+      if (k > 0) {  // SaveGameState{cell, f}
+        ctx.nonce = nonce + static_cast<uint32_t>(k);
+        const CS cval = (p.debug & 4u) ? CS{} : G::checksum(w, f, lane, ctx);
+        const unsigned slot = slot_of(f);
+        if (!(p.debug & 2u)) store_words<NW>(p.snap + slot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), w);
+        if (lead) csa[slot * Spad + s] = cval;
+        if (k == CD) {
+          if (lead) fsa[slot * Spad + s] = cval;  // first save of frame c: first-seen
+          recorded = cval;
+        } else if (cval != fsw[k - 1]) {
+          mismatch = f;  // newest mismatching frame wins
+        }
+        // Same lane, same address, program order: this load returns the cell just stored.
+        if (k == 1 && more)
+          load_words<NW>(p.snap + slot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), wn);
+      }
+      if (p.debug & 1u)
+        w[0] += win[k];
+      else
+        G::advance(w, (p.debug & 32u) ? static_cast<InRec>(win[k] & static_cast<InRec>(p.debug >> 8)) : win[k], lane, 0u,
+                   &p.counters[1]);  // AdvanceFrame{inputs}
+      if ((f + 1) % 100 == 0) {  // ex_game periodic_checksum (frame % CHECKSUM_PERIOD == 0)
+        ctx.nonce = nonce + 128u + static_cast<uint32_t>(k);
+        const CS cval = G::checksum(w, f + 1, lane, ctx);
+        if (G::kDisplay && lead) reinterpret_cast<CS*>(p.periodic_cs)[s] = cval;
+      }
+    }
+    if constexpr (G::kDisplay) {  // Game::last_checksum after the final AdvanceFrame
+      ctx.nonce = nonce + 255u;
+      const CS cval = G::checksum(w, c + 1, lane, ctx);
+      if (lead) reinterpret_cast<CS*>(p.last_cs)[s] = cval;
+    }
+    if (mismatch != kNullFrame && !p.debug) {  // experiments (debug knobs) change results: never freeze
+      store_words<NW>(p.live, static_cast<int>(Gpad), static_cast<int>(g), w);
+      if (lead) {
+        p.err[s] = mismatch;
+        p.live_frame[s] = c + 1;
+        atomicOr(&p.frozen[s >> 6], 1ull << (s & 63));
+        atomicAdd(&p.counters[0], 1u);
+      }
+      return;  // advance_frame returns Err for this session from the next tick on
+    }
+    if (!more) {
+      if (p.live_out_last) store_words<NW>(p.live, static_cast<int>(Gpad), static_cast<int>(g), w);
+      break;
+    }
+    // ---- wait here, inside the iteration, for the loads the next tick uses.
+    // Left to the loop back-edge, the compiler's wait for them would also
+    // cover every store issued after them (it loses the count across the edge).
+    settle(static_cast<uint32_t>(newin_next));
+    settle(static_cast<uint32_t>(next_last));
+#pragma unroll
+    for (int i = 0; i < NW; ++i) settle(wn[i]);
+    // ---- slide the windows to the next tick (c+1): f0 -> f0+1
+#pragma unroll
+    for (int k = 0; k < CD; ++k) win[k] = win[k + 1];
+    win[CD] = next_last;
+    newin = newin_next;
+#pragma unroll
+    for (int k = 0; k + 1 < NF; ++k) fsw[k] = fsw[k + 1];
+    if (CD > 1) fsw[NF - 1] = recorded;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) w[i] = wn[i];
+    f0 += 1;
+  }
+}
+
+template <class G>
+__global__ void report_kernel(const typename G::CS* __restrict__ cs, const int32_t* __restrict__ err, int S,
+                              int32_t frame, rb_checksum_report* __restrict__ out) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= S) return;
+  const U128 c = to_u128(cs[s]);
+  rb_checksum_report r;
+  r.checksum_lo = c.lo;
+  r.checksum_hi = c.hi;
+  r.frame = frame;
+  r.mismatch_frame = err[s];
+  out[s] = r;
+}
+
+struct GameOps {
+  virtual ~GameOps() = default;
+  int nw = 0, lanes = 1, players = 0, input_bytes = 0, inrec_bytes = 0, cs_bytes = 0, image_bytes = 0, canon_words = 0;
+  bool display = false;
+  virtual void word_loc(int k, int* lane, int* word) const = 0;
+  virtual void init_words(uint32_t* w) const = 0;
+  virtual void image(const uint32_t* w, int32_t frame, uint8_t* out) const = 0;
+  virtual U128 cs_at(const void* arr, size_t i) const = 0;
+  virtual hipError_t launch_tick(const KParams& p, int block, hipStream_t st) const = 0;
+  // fused steady-state ticks; hipErrorNotSupported when CD has no instantiation
+  virtual hipError_t launch_steady(const RunParams& p, int cd, int block, hipStream_t st) const = 0;
+  bool launch_steady_supported(int cd) const { return cd >= 1 && cd <= 8; }
+  virtual hipError_t launch_report(const void* cs, const int32_t* err, int S, int32_t frame, void* out,
+                                   hipStream_t st) const = 0;
+};
+
+template <class G>
+struct GameOpsT final : GameOps {
+  GameOpsT() {
+    nw = G::NWL;
+    lanes = G::kLanes;
+    canon_words = G::kCanonWords;
+    players = G::kPlayers;
+    input_bytes = G::kInputBytes;
+    inrec_bytes = sizeof(typename G::InRec);
+    cs_bytes = sizeof(typename G::CS);
+    image_bytes = G::kImageBytes;
+    display = G::kDisplay;
+  }
+  void word_loc(int k, int* lane, int* word) const override { G::word_loc(k, lane, word); }
+  void init_words(uint32_t* w) const override { G::init(w); }
+  void image(const uint32_t* w, int32_t frame, uint8_t* out) const override { G::image(w, frame, out); }
+  U128 cs_at(const void* arr, size_t i) const override {
+    return to_u128(reinterpret_cast<const typename G::CS*>(arr)[i]);
+  }
+  hipError_t launch_tick(const KParams& p, int block, hipStream_t st) const override {
+    const int grid = (p.Spad * G::kLanes + block - 1) / block;
+    if (p.in_mode == 2)
+      hipLaunchKernelGGL((tick_kernel<G, true>), dim3(grid), dim3(block), 0, st, p);
+    else
+      hipLaunchKernelGGL((tick_kernel<G, false>), dim3(grid), dim3(block), 0, st, p);
+    return hipGetLastError();
+  }
+  template <int CD>
+  static hipError_t steady_cd(const RunParams& p, int block, hipStream_t st) {
+    const int grid = (p.Spad * G::kLanes + block - 1) / block;
+    hipLaunchKernelGGL((steady_kernel<G, CD>), dim3(grid), dim3(block), 0, st, p);
+    return hipGetLastError();
+  }
+  hipError_t launch_steady(const RunParams& p, int cd, int block, hipStream_t st) const override {
+    switch (cd) {
+      case 1: return steady_cd<1>(p, block, st);
+      case 2: return steady_cd<2>(p, block, st);
+      case 3: return steady_cd<3>(p, block, st);
+      case 4: return steady_cd<4>(p, block, st);
+      case 5: return steady_cd<5>(p, block, st);
+      case 6: return steady_cd<6>(p, block, st);
+      case 7: return steady_cd<7>(p, block, st);
+      case 8: return steady_cd<8>(p, block, st);
+      default: return hipErrorNotSupported;
+    }
+  }
+  hipError_t launch_report(const void* cs, const int32_t* err, int S, int32_t frame, void* out,
+                           hipStream_t st) const override {
+    hipLaunchKernelGGL(report_kernel<G>, dim3((S + 255) / 256), dim3(256), 0, st,
+                       reinterpret_cast<const typename G::CS*>(cs), err, S, frame,
+                       reinterpret_cast<rb_checksum_report*>(out));
+    return hipGetLastError();
+  }
+};
+
+
+// per-translation-unit factories (ops_*.hip); nullptr for an unsupported player count
+std::unique_ptr<GameOps> make_exgame_ops(int players, bool lane_per_session);
+std::unique_ptr<GameOps> make_brawler_ops(int players);
+std::unique_ptr<GameOps> make_stub_ops(int game, int players);
+
+}  // namespace rb

@@ -1,0 +1,19 @@
+// ggrs_amd/csrc/ops_exgame.hip — device code of examples/ex_game (kernels.hpp
+// instantiated for ExGame<P, lane-per-player | lane-per-session>).
+#include "kernels.hpp"
+
+namespace rb {
+template <bool kSplit>
+static std::unique_ptr<GameOps> make_ex_game(int players) {
+  switch (players) {
+    case 1: return std::make_unique<GameOpsT<ExGame<1, kSplit>>>();
+    case 2: return std::make_unique<GameOpsT<ExGame<2, kSplit>>>();
+    case 3: return std::make_unique<GameOpsT<ExGame<3, kSplit>>>();
+    case 4: return std::make_unique<GameOpsT<ExGame<4, kSplit>>>();
+    default: return nullptr;
+  }
+}
+std::unique_ptr<GameOps> make_exgame_ops(int players, bool lane_per_session) {
+  return lane_per_session ? make_ex_game<false>(players) : make_ex_game<true>(players);
+}
+}  // namespace rb
