@@ -31,18 +31,15 @@ METRIC = "session-frames resimulated/sec (node) at 8-frame rollback; % HBM roofl
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
-def algorithmic_bytes_per_session_tick(P: int, cd: int, nw: int, cs_bytes: int, in_rec: int, in_bytes: int,
-                                       display: bool = True) -> int:
-    """Bytes one steady-state tick must move per session:
-    1 snapshot load (LoadGameState) + cd snapshot saves, cd cell checksums
-    written, the first-seen record of frame c written, the tick's new inputs
-    read and written to the input ring, the input of the window's newest frame
-    read, and the display checksum written (ex_game).  First-seen values and
-    inputs of older frames are carried in registers across the fused ticks
-    (steady_kernel), so they are not counted."""
-    state = 4 * nw
-    return (state * (1 + cd) + cs_bytes * cd + cs_bytes + P * in_bytes + in_rec + P * in_bytes
-            + (cs_bytes if display else 0))
+def algorithmic_bytes_per_session_tick(P: int, cd: int, nw: int, cs_bytes: int, in_bytes: int) -> int:
+    """Bytes one steady-state tick must move per session: SURVEY.md section 8(d)
+    B_tick = S_state * (1 load + cd saves) + cd * cs_bytes * 2 (checksum written
+    + first-seen checksum read) + (cd + 1) * P * in_bytes (the inputs of every
+    AdvanceFrame) + 4 (session status word).  S_state = 4 * nw: the per-session
+    frame word is implicit (the batch-uniform cell tag).
+    Values the fused kernel carries in registers across ticks still count: the
+    figure is the algorithm's, not the implementation's."""
+    return 4 * nw * (1 + cd) + cd * cs_bytes * 2 + (cd + 1) * P * in_bytes + 4
 
 
 def cpu_baseline(args, P):
@@ -195,12 +192,10 @@ def main():
         assert timed_ticks == args.steps, (timed_ticks, args.steps)
         avg_kernel_s = kernel_ms / 1e3 / max(1, launches)  # per steady_kernel launch
         ticks_per_launch = timed_ticks / max(1, launches)
-        in_rec = 2 if P == 2 else (1 if P == 1 else 4)
         # device words of one session's state: ex_game 5 f32 per player (frame
         # word implicit); brawler 256 entities x 8 i32
         nw = 256 * 8 if brawler else 5 * P
-        bpt = algorithmic_bytes_per_session_tick(P, cd, nw=nw, cs_bytes=2, in_rec=in_rec, in_bytes=1,
-                                                 display=not brawler)
+        bpt = algorithmic_bytes_per_session_tick(P, cd, nw=nw, cs_bytes=2, in_bytes=1)
         bytes_per_launch = bpt * S * ticks_per_launch
         achieved = bytes_per_launch / avg_kernel_s / 1e9
         cfg_key = f"{args.game} P={P} cd={cd} W={args.max_prediction} d={args.input_delay} S={S}"

@@ -10,7 +10,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libggrs_amd.so")
+# GGRS_AMD_LIB: load another build of the same library (kernel experiments, tools/)
+LIB_PATH = os.environ.get("GGRS_AMD_LIB") or os.path.join(_HERE, "libggrs_amd.so")
 
 RB_ABI_VERSION = 1
 RB_NULL_FRAME = -1
@@ -89,6 +90,7 @@ SIGNATURES = [
     ("rb_export_checksum_report", _I32, [_P, _I32, _P]),
     ("rb_debug_corrupt_cell", _I32, [_P, _I32, _I32, _I32, ctypes.c_uint32]),
     ("rb_debug_sincosf", _I32, [_I32, _P, _P, _P, ctypes.c_int64]),
+    ("rb_debug_speed_clamp", _I32, [_I32, _P, _P, _P, _P, ctypes.c_int64]),
     ("rb_profile_enable", _I32, [_P, _I32]),
     ("rb_profile_take", _I32, [_P, ctypes.POINTER(ctypes.c_double), _PI32]),
 ]

@@ -68,21 +68,27 @@ __device__ __noinline__ SinCos sincosf_large(float y, uint32_t* unexpected) {
 
 __device__ __forceinline__ SinCos sincosf_glibc(float y, uint32_t* unexpected) {
   // |y| < pi/4 takes glibc's unreduced branch: reduce_fast yields n = 0 and
-  // xr = y exactly there, so one straight-line path serves both; |y| < 2^-12
-  // returns (y, 1) as glibc does.
+  // xr = y exactly there, so one straight-line path serves both.
   const double hpi_inv = 0x1.45F306DC9C883p+23, hpi = 0x1.921FB54442D18p0;  // !TOINT_INTRINSICS form (x86_64)
   const double x = y;
   const int n = (static_cast<int32_t>(x * hpi_inv) + 0x800000) >> 24;
-  const double xr = __builtin_fma(-static_cast<double>(n), hpi, x);
-  const double xs = ((n & 3) == 1 || (n & 3) == 2) ? -xr : xr;  // sign[4] = {1,-1,-1,1}
+  double xr = __builtin_fma(-static_cast<double>(n), hpi, x);
   const double x2 = xr * xr;
-  const float sp = static_cast<float>(sin_poly(xs, x2));
-  const double cpd = cos_poly(x2);
-  const float cp = static_cast<float>((n & 2) ? -cpd : cpd);  // __sincosf_table[1]
+  // sign[4] = {1,-1,-1,1}: negate when (n & 3) is 1 or 2, i.e. bit 1 of n + 1.
+  // Adding 2^31 to the high word flips the sign bit (no carry out of bit 31).
+  const uint32_t sflip = (static_cast<uint32_t>(n + 1) >> 1) & 1u;
+  xr = __hiloint2double(static_cast<int>(static_cast<uint32_t>(__double2hiint(xr)) + (sflip << 31)), __double2loint(xr));
+  const float sp = static_cast<float>(sin_poly(xr, x2));
+  // __sincosf_table[1] (n & 2) negates every cosine coefficient: negate the
+  // rounded result (rounding is sign-symmetric).
+  const uint32_t cflip = (static_cast<uint32_t>(n) >> 1) & 1u;
+  const float cp = __uint_as_float(__float_as_uint(static_cast<float>(cos_poly(x2))) + (cflip << 31));
   SinCos r;
   // sinf: n even -> sine poly, odd -> cosine poly; cosf uses n ^ 1.
   r.s = (n & 1) ? cp : sp;
   r.c = (n & 1) ? sp : cp;
+  // |y| < 2^-12: glibc returns (y, 1).  Inline: ex_game's rotations sit at
+  // exactly 0 for long stretches (State::new gives player 1 rot = 0).
   const uint32_t top = abstop12(y);
   if (top < abstop12(0x1p-12f)) {
     r.s = y;
@@ -119,8 +125,17 @@ __host__ __device__ constexpr uint32_t fl16_weights(int n, int o) {
   return static_cast<uint32_t>(n - o) | (static_cast<uint32_t>(n - o - 1) << 8) |
          (static_cast<uint32_t>(n - o - 2) << 16) | (static_cast<uint32_t>(n - o - 3) << 24);
 }
+// x mod 255 for x < 2^24, valid in the low 8 bits only: q = floor(x / 255)
+// by a multiply-high; x - 255 q = x + 0xFF01 q (mod 2^16) is one v_mad_u32_u24.
+__device__ __forceinline__ uint32_t mod255_lo8(uint32_t x) {
+  const uint32_t q = __umulhi(x, 0x80808081u) >> 7;
+  return __umul24(q, 0xFF01u) + x;
+}
+// Both sums must be < 2^24: images of n bytes with 255 * n * (n + 1) / 2 < 2^24
+// (n <= 361; ex_game images are at most 116 bytes).
 __device__ __forceinline__ uint16_t fl16_finish(const Fl16& a) {
-  return static_cast<uint16_t>(((a.s2 % 255u) << 8) | (a.s1 % 255u));
+  // (s2 mod 255) << 8 | (s1 mod 255): byte 0 of each, packed by one v_perm_b32
+  return static_cast<uint16_t>(__builtin_amdgcn_perm(mod255_lo8(a.s2), mod255_lo8(a.s1), 0x0c0c0400u));
 }
 
 // ----------------------------------------------------------------------------

@@ -41,6 +41,16 @@ __global__ void sincos_kernel(const float* __restrict__ x, float* __restrict__ s
   co[i] = r.c;
 }
 
+__global__ void clamp_kernel(const float* __restrict__ vx, const float* __restrict__ vy, float* __restrict__ ox,
+                             float* __restrict__ oy, int64_t n) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float a = vx[i], b = vy[i];
+  ExGame<1, false>::speed_clamp(a, b);
+  ox[i] = a;
+  oy[i] = b;
+}
+
 inline std::unique_ptr<GameOps> make_game(int game, int players, bool lane_per_session) {
   switch (game) {
     case RB_GAME_EX_GAME: return make_exgame_ops(players, lane_per_session);
@@ -726,31 +736,55 @@ rb_status rb_debug_corrupt_cell(rb_batch* b, int32_t session, int32_t frame, int
   return RB_OK;
 }
 
-rb_status rb_debug_sincosf(int32_t device, const float* x, float* so, float* co, int64_t n) {
-  rb_batch* b = nullptr;
+}  // extern "C"
+
+// Element-wise device evaluation for the parity tests: (a[i], b[i]) -> (o1[i], o2[i]).
+template <class Launch>
+static rb_status debug_map2(const char* what, int32_t device, const float* a, const float* b, float* o1, float* o2,
+                            int64_t n, Launch launch) {
+  rb_batch* none = nullptr;
   if (n <= 0) return RB_OK;
-  HIP_TRY(b, hipSetDevice(device));
-  float *dx = nullptr, *ds = nullptr, *dc = nullptr;
+  HIP_TRY(none, hipSetDevice(device));
+  float *da = nullptr, *db = nullptr, *d1 = nullptr, *d2 = nullptr;
   uint32_t* du = nullptr;
   const size_t bytes = static_cast<size_t>(n) * 4;
-  hipError_t e = hipMalloc(&dx, bytes);
-  if (e == hipSuccess) e = hipMalloc(&ds, bytes);
-  if (e == hipSuccess) e = hipMalloc(&dc, bytes);
+  hipError_t e = hipMalloc(&da, bytes);
+  if (e == hipSuccess) e = hipMalloc(&db, bytes);
+  if (e == hipSuccess) e = hipMalloc(&d1, bytes);
+  if (e == hipSuccess) e = hipMalloc(&d2, bytes);
   if (e == hipSuccess) e = hipMalloc(&du, 4);
   if (e == hipSuccess) e = hipMemset(du, 0, 4);
-  if (e == hipSuccess) e = hipMemcpy(dx, x, bytes, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(da, a, bytes, hipMemcpyHostToDevice);
+  if (e == hipSuccess && b) e = hipMemcpy(db, b, bytes, hipMemcpyHostToDevice);
   if (e == hipSuccess) {
-    hipLaunchKernelGGL(sincos_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, nullptr, dx, ds, dc, n, du);
+    launch(dim3(static_cast<unsigned>((n + 255) / 256)), da, db, d1, d2, du);
     e = hipGetLastError();
   }
-  if (e == hipSuccess) e = hipMemcpy(so, ds, bytes, hipMemcpyDeviceToHost);
-  if (e == hipSuccess) e = hipMemcpy(co, dc, bytes, hipMemcpyDeviceToHost);
-  (void)hipFree(dx);
-  (void)hipFree(ds);
-  (void)hipFree(dc);
+  if (e == hipSuccess) e = hipMemcpy(o1, d1, bytes, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(o2, d2, bytes, hipMemcpyDeviceToHost);
+  (void)hipFree(da);
+  (void)hipFree(db);
+  (void)hipFree(d1);
+  (void)hipFree(d2);
   (void)hipFree(du);
-  if (e != hipSuccess) return fail(nullptr, RB_DEVICE_ERROR, std::string("rb_debug_sincosf: ") + hipGetErrorString(e));
+  if (e != hipSuccess) return fail(nullptr, RB_DEVICE_ERROR, std::string(what) + ": " + hipGetErrorString(e));
   return RB_OK;
+}
+
+extern "C" {
+
+rb_status rb_debug_sincosf(int32_t device, const float* x, float* so, float* co, int64_t n) {
+  return debug_map2("rb_debug_sincosf", device, x, nullptr, so, co, n,
+                    [n](dim3 grid, float* da, float*, float* d1, float* d2, uint32_t* du) {
+                      hipLaunchKernelGGL(sincos_kernel, grid, dim3(256), 0, nullptr, da, d1, d2, n, du);
+                    });
+}
+
+rb_status rb_debug_speed_clamp(int32_t device, const float* vx, const float* vy, float* ox, float* oy, int64_t n) {
+  return debug_map2("rb_debug_speed_clamp", device, vx, vy, ox, oy, n,
+                    [n](dim3 grid, float* da, float* db, float* d1, float* d2, uint32_t*) {
+                      hipLaunchKernelGGL(clamp_kernel, grid, dim3(256), 0, nullptr, da, db, d1, d2, n);
+                    });
 }
 
 rb_status rb_profile_enable(rb_batch* b, int32_t on) {

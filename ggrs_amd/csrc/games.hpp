@@ -74,6 +74,7 @@ struct ExGame {
   static constexpr int NWL = 5 * kPlayersPerLane;  // per player: x, y, vx, vy, rot
   static constexpr int kInputBytes = 1;
   static constexpr int kImageBytes = 36 + 20 * P;  // bincode 1.3 image of State (ex_game.rs:224-231)
+  static_assert(255 * kImageBytes * (kImageBytes + 1) / 2 < (1 << 24), "fl16_finish needs sums < 2^24");
   static constexpr bool kDisplay = true;           // Game::last_checksum / periodic_checksum
   using InRec = typename InRecOf<P>::T;
   using CS = uint16_t;
@@ -143,6 +144,21 @@ struct ExGame {
 
   __device__ static uint32_t player_input(InRec rec, int i) { return (static_cast<uint32_t>(rec) >> (8 * i)) & 0xffu; }
 
+  // ex_game.rs:300-304: if |v| > MAX_SPEED { v = v * MAX_SPEED / |v| }.
+  __device__ static void speed_clamp(float& vx, float& vy) {
+    // mag > 7 <=> vx^2+vy^2 > 49: sqrt is correctly rounded and monotone,
+    // sqrt(49) = 7 exactly, and the next float above 49 (49 + 2^-18) has a
+    // square root that rounds above 7 (tests/test_oracle.py checks both
+    // sides), NaN compares false both ways.  The sqrt is only needed for
+    // the clamp, so it moves inside the branch.
+    const float m2 = vx * vx + vy * vy;
+    if (m2 > kMaxSpeed * kMaxSpeed) {
+      const float mag = __builtin_sqrtf(m2);
+      vx = (vx * kMaxSpeed) / mag;
+      vy = (vy * kMaxSpeed) / mag;
+    }
+  }
+
   // State::advance (ex_game.rs:259-321) for one player.  Compiled with
   // -ffp-contract=off: every f32 operation rounds exactly as the reference's.
   __device__ static void advance_player(uint32_t* w, uint32_t input, uint32_t* unexpected) {
@@ -159,11 +175,7 @@ struct ExGame {
       vy = up ? vy + ty : vy - ty;
     }
     if (left != right) rot = rem_euclid(left ? rot - kRotationSpeed : rot + kRotationSpeed, 2.0f * kPi);
-    const float mag = __builtin_sqrtf(vx * vx + vy * vy);
-    if (mag > kMaxSpeed) {
-      vx = (vx * kMaxSpeed) / mag;
-      vy = (vy * kMaxSpeed) / mag;
-    }
+    speed_clamp(vx, vy);
     float x = old_x + vx, y = old_y + vy;
     x = fminf(fmaxf(x, 0.0f), kWidth);
     y = fminf(fmaxf(y, 0.0f), kHeight);

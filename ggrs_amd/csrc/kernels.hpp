@@ -318,10 +318,23 @@ struct RunParams {
 // An empty asm that reads v: the compiler must complete the load that
 // produced v before this point (an s_waitcnt counted within the iteration).
 __device__ __forceinline__ void settle(uint32_t v) { asm volatile("" ::"v"(v)); }
+__device__ __forceinline__ void settle(uint64_t v) {
+  settle(static_cast<uint32_t>(v));
+  settle(static_cast<uint32_t>(v >> 32));
+}
+__device__ __forceinline__ void settle(U128 v) {
+  settle(v.lo);
+  settle(v.hi);
+}
+__device__ __forceinline__ void settle(uint16_t v) { settle(static_cast<uint32_t>(v)); }
+__device__ __forceinline__ void settle(uint8_t v) { settle(static_cast<uint32_t>(v)); }
 
-template <class G, int CD>
+// kExp: attribution experiments (RunParams::debug knobs, tools/exp_steady.py);
+// instantiated only in builds made with RB_EXPERIMENTS=1, never in the product.
+template <class G, int CD, bool kExp>
 __global__ void __launch_bounds__(256) steady_kernel(const RunParams p) {
   static_assert(CD >= 1, "steady shape needs a rollback");
+  const uint32_t dbg = kExp ? p.debug : 0u;
   using InRec = typename G::InRec;
   using CS = typename G::CS;
   constexpr int NW = G::NWL;
@@ -344,6 +357,11 @@ __global__ void __launch_bounds__(256) steady_kernel(const RunParams p) {
   CS* __restrict__ fsa = reinterpret_cast<CS*>(p.fs);
   const int W = p.W;
   auto slot_of = [W](int f) { return static_cast<unsigned>(f % W); };
+  // slot of frame f0 + k given slot0 = f0 % W, k <= CD < W: no division per step
+  auto slot_after = [W](unsigned slot0, int k) {
+    const unsigned sl = slot0 + static_cast<unsigned>(k);
+    return sl >= static_cast<unsigned>(W) ? sl - static_cast<unsigned>(W) : sl;
+  };
   // The new inputs of launch tick tt (the read-only per-tick input buffer).
   auto new_input = [&](int tt) -> InRec {
     const uint8_t* tin = p.in_base + static_cast<int64_t>(tt) * p.in_stride;
@@ -389,6 +407,19 @@ __global__ void __launch_bounds__(256) steady_kernel(const RunParams p) {
   // retires loads and stores in issue order), so every input load is issued
   // one tick before it is used, ahead of that tick's stores.
   InRec newin = new_input(0);
+  unsigned slot0 = slot_of(f0);  // f0 % W, advanced with f0
+  // Complete the prologue loads before the loop.  The waitcnt pass merges
+  // the loop header's state from the preheader and the latch: a load still
+  // pending on the preheader path makes it put a conservative vmcnt at the
+  // first use inside the loop, which in the steady state then waits for every
+  // store of the previous tick.
+#pragma unroll
+  for (int i = 0; i < NW; ++i) settle(w[i]);
+#pragma unroll
+  for (int k = 0; k <= CD; ++k) settle(win[k]);
+#pragma unroll
+  for (int k = 0; k + 1 < CD; ++k) settle(fsw[k]);
+  settle(newin);
   for (int t = 0; t < p.T; ++t) {
     const int c = p.c0 + t;
     const bool more = t + 1 < p.T;
@@ -408,9 +439,9 @@ __global__ void __launch_bounds__(256) steady_kernel(const RunParams p) {
       const int f = f0 + k;
       if (k > 0) {  // SaveGameState{cell, f}
         ctx.nonce = nonce + static_cast<uint32_t>(k);
-        const CS cval = (p.debug & 4u) ? CS{} : G::checksum(w, f, lane, ctx);
-        const unsigned slot = slot_of(f);
-        if (!(p.debug & 2u)) store_words<NW>(p.snap + slot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), w);
+        const CS cval = (dbg & 4u) ? CS{} : G::checksum(w, f, lane, ctx);
+        const unsigned slot = slot_after(slot0, k);
+        if (!(dbg & 2u)) store_words<NW>(p.snap + slot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), w);
         if (lead) csa[slot * Spad + s] = cval;
         if (k == CD) {
           if (lead) fsa[slot * Spad + s] = cval;  // first save of frame c: first-seen
@@ -422,10 +453,10 @@ __global__ void __launch_bounds__(256) steady_kernel(const RunParams p) {
         if (k == 1 && more)
           load_words<NW>(p.snap + slot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), wn);
       }
-      if (p.debug & 1u)
+      if (dbg & 1u)
         w[0] += win[k];
       else
-        G::advance(w, (p.debug & 32u) ? static_cast<InRec>(win[k] & static_cast<InRec>(p.debug >> 8)) : win[k], lane, 0u,
+        G::advance(w, (dbg & 32u) ? static_cast<InRec>(win[k] & static_cast<InRec>(dbg >> 8)) : win[k], lane, 0u,
                    &p.counters[1]);  // AdvanceFrame{inputs}
       if ((f + 1) % 100 == 0) {  // ex_game periodic_checksum (frame % CHECKSUM_PERIOD == 0)
         ctx.nonce = nonce + 128u + static_cast<uint32_t>(k);
@@ -438,7 +469,7 @@ __global__ void __launch_bounds__(256) steady_kernel(const RunParams p) {
       const CS cval = G::checksum(w, c + 1, lane, ctx);
       if (lead) reinterpret_cast<CS*>(p.last_cs)[s] = cval;
     }
-    if (mismatch != kNullFrame && !p.debug) {  // experiments (debug knobs) change results: never freeze
+    if (mismatch != kNullFrame && !dbg) {  // experiments (debug knobs) change results: never freeze
       store_words<NW>(p.live, static_cast<int>(Gpad), static_cast<int>(g), w);
       if (lead) {
         p.err[s] = mismatch;
@@ -470,6 +501,7 @@ __global__ void __launch_bounds__(256) steady_kernel(const RunParams p) {
 #pragma unroll
     for (int i = 0; i < NW; ++i) w[i] = wn[i];
     f0 += 1;
+    slot0 = slot_after(slot0, 1);
   }
 }
 
@@ -533,7 +565,15 @@ struct GameOpsT final : GameOps {
   template <int CD>
   static hipError_t steady_cd(const RunParams& p, int block, hipStream_t st) {
     const int grid = (p.Spad * G::kLanes + block - 1) / block;
-    hipLaunchKernelGGL((steady_kernel<G, CD>), dim3(grid), dim3(block), 0, st, p);
+    if (p.debug) {
+#if RB_EXPERIMENTS
+      hipLaunchKernelGGL((steady_kernel<G, CD, true>), dim3(grid), dim3(block), 0, st, p);
+      return hipGetLastError();
+#else
+      return hipErrorNotSupported;  // experiment knobs need a RB_EXPERIMENTS=1 build
+#endif
+    }
+    hipLaunchKernelGGL((steady_kernel<G, CD, false>), dim3(grid), dim3(block), 0, st, p);
     return hipGetLastError();
   }
   hipError_t launch_steady(const RunParams& p, int cd, int block, hipStream_t st) const override {

@@ -14,6 +14,11 @@ static std::unique_ptr<GameOps> make_ex_game(int players) {
   }
 }
 std::unique_ptr<GameOps> make_exgame_ops(int players, bool lane_per_session) {
+#if RB_EXGAME_P2_ONLY  // kernel-experiment builds (tools/): the bench configuration only
+  if (players == 2 && !lane_per_session) return std::make_unique<GameOpsT<ExGame<2, true>>>();
+  return nullptr;
+#else
   return lane_per_session ? make_ex_game<false>(players) : make_ex_game<true>(players);
+#endif
 }
 }  // namespace rb

@@ -182,6 +182,12 @@ rb_status rb_debug_corrupt_cell(rb_batch* b, int32_t session, int32_t frame, int
  * libm in the parity tests. */
 rb_status rb_debug_sincosf(int32_t device, const float* x, float* sin_out, float* cos_out, int64_t n);
 
+/* Device evaluation of ex_game's speed clamp (ex_game.rs:300-304: v * MAX_SPEED
+ * / |v| when |v| > MAX_SPEED) for n host (vx, vy) pairs — pins the short exact
+ * sqrt/division sequences of device_math.hpp against host IEEE arithmetic. */
+rb_status rb_debug_speed_clamp(int32_t device, const float* vx, const float* vy, float* vx_out, float* vy_out,
+                               int64_t n);
+
 /* HIP event timing of the tick kernel on the batch's stream, for bench.py:
  * rb_profile_enable(b, k) brackets every k-th single-tick launch (k <= 1:
  * every 8th) and every fused rb_run_ticks launch with an event pair;

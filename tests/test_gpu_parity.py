@@ -94,6 +94,39 @@ def test_device_sincosf_bit_exact_with_glibc(gpu_available):
     assert bad_c.size == 0, (x[bad_c[:5]], gc[bad_c[:5]], hc[bad_c[:5]])
 
 
+def test_device_speed_clamp_bit_exact(gpu_available):
+    # ex_game.rs:300-304 evaluated with host IEEE f32 (numpy rounds each op)
+    # against the device clamp: the short sqrt/division sequences for the
+    # normal range and the full ones outside it.
+    import ctypes
+    from ggrs_amd import _lib as L
+    rng = np.random.default_rng(11)
+    n = 1 << 22
+    ang = rng.uniform(0, 2 * np.pi, n)
+    mag = np.concatenate([rng.uniform(6.9, 7.6, n // 2), np.exp(rng.uniform(np.log(7), np.log(1e30), n // 2))])
+    vx = (mag * np.cos(ang)).astype(np.float32)
+    vy = (mag * np.sin(ang)).astype(np.float32)
+    # edge operands: zeros of either sign, tiny/denormal components, huge, inf, nan
+    ex = np.array([0.0, -0.0, 1e-30, -1e-40, 7.0, 7.0000005, 1e19, 3e38, np.inf, -np.inf, np.nan, 4.95, -4.95], np.float32)
+    gx, gy = np.meshgrid(ex, ex)
+    vx = np.concatenate([vx, gx.ravel(), rng.integers(0, 1 << 32, 1 << 16, dtype=np.uint64).astype(np.uint32).view(np.float32)])
+    vy = np.concatenate([vy, gy.ravel(), rng.integers(0, 1 << 32, 1 << 16, dtype=np.uint64).astype(np.uint32).view(np.float32)])
+    ox = np.empty_like(vx)
+    oy = np.empty_like(vy)
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    assert L.load().rb_debug_speed_clamp(0, p(vx), p(vy), p(ox), p(oy), vx.size) == 0
+    seven = np.float32(7.0)
+    with np.errstate(all="ignore"):
+        m = np.sqrt(vx * vx + vy * vy)
+        c = m > seven
+        hx = np.where(c, (vx * seven) / m, vx).astype(np.float32)
+        hy = np.where(c, (vy * seven) / m, vy).astype(np.float32)
+    assert c.sum() > n // 2
+    for got, want in ((ox, hx), (oy, hy)):
+        bad = np.nonzero((got.view(np.uint32) != want.view(np.uint32)) & ~(np.isnan(got) & np.isnan(want)))[0]
+        assert bad.size == 0, (vx[bad[:5]], vy[bad[:5]], got[bad[:5]], want[bad[:5]])
+
+
 # ---------------------------------------------------------------------------- ex_game
 @pytest.mark.parametrize("P,W,cd,d", [(2, 8, 7, 2), (2, 8, 2, 0), (2, 8, 0, 0), (2, 8, 1, 0), (1, 8, 3, 1),
                                       (3, 8, 5, 2), (4, 8, 7, 2), (2, 9, 8, 0), (2, 16, 12, 3)])

@@ -121,3 +121,17 @@ def test_oracle_brawler_synctest_runs_and_exercises_the_rules():
     assert (ent[:, :P, 7] > 0).any(), "no player took damage"
     assert (ent[:, P:, 4] < 100).any(), "no AI entity took damage"
     assert (ent[:, P:, 7] > 0).all() or (ent[:, P:, 4] <= 0).any()
+
+
+def test_speed_clamp_compare_without_sqrt():
+    # games.hpp ExGame::advance_player tests `vx*vx + vy*vy > 49` where the
+    # reference tests `sqrt(vx*vx + vy*vy) > 7` (ex_game.rs:300-304).  f32 sqrt
+    # is correctly rounded (numpy too), so check the equivalence on every float
+    # in [40, 60) and on a log-uniform sample of the whole range.
+    lo, hi = np.float32(40.0).view(np.uint32), np.float32(60.0).view(np.uint32)
+    m2 = np.arange(lo, hi, dtype=np.uint32).view(np.float32)
+    rng = np.random.default_rng(7)
+    m2 = np.concatenate([m2, rng.integers(0, 0x7F800000, 1 << 20, dtype=np.uint32).view(np.float32),
+                         np.array([0.0, 49.0, np.inf, np.nan], np.float32)])
+    with np.errstate(invalid="ignore"):
+        assert ((np.sqrt(m2) > np.float32(7.0)) == (m2 > np.float32(49.0))).all()

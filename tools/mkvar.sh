@@ -1,0 +1,13 @@
+#!/bin/bash
+# Kernel experiments: build ggrs_amd/var/lib_<name>.so = the product library with
+# ops_exgame.hip recompiled under extra -D flags (bench configuration only,
+# RB_EXGAME_P2_ONLY); tools/varrun.sh benches them via GGRS_AMD_LIB.
+# usage: tools/mkvar.sh <name> [-DFOO=1 ...]   (after a normal make)
+# build variant libs: name + defines
+set -e
+cd "$(dirname "$0")/../ggrs_amd/csrc"
+F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -DRB_EXPERIMENTS=0"
+name=$1; shift
+mkdir -p build/var
+/opt/rocm/bin/hipcc $F "$@" -DRB_EXGAME_P2_ONLY=1 -c -o build/var/ex_$name.o ops_exgame.hip
+/opt/rocm/bin/hipcc $F -shared -o ../var/lib_$name.so build/engine.o build/var/ex_$name.o build/ops_brawler.o build/ops_stub.o
