@@ -25,5 +25,6 @@ from .session import (  # noqa: F401
     decode_ex_game,
 )
 from .synth import SEED, synth_inputs  # noqa: F401
+from .p2p import P2PSession, PlayerType, synth_network  # noqa: F401
 
 __version__ = "0.1.0"

@@ -54,6 +54,24 @@ class RbConfig(ctypes.Structure):
     ]
 
 
+class RbP2PConfig(ctypes.Structure):
+    _fields_ = [
+        ("abi_version", ctypes.c_int32),
+        ("game", ctypes.c_int32),
+        ("num_sessions", ctypes.c_int32),
+        ("num_players", ctypes.c_int32),
+        ("max_prediction", ctypes.c_int32),
+        ("input_delay", ctypes.c_int32),
+        ("device", ctypes.c_int32),
+        ("local_mask", ctypes.c_uint32),
+        ("remote_delay", ctypes.c_int32),
+        ("sparse_saving", ctypes.c_int32),
+        ("flags", ctypes.c_uint32),
+        ("block_size", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32 * 4),
+    ]
+
+
 class RbChecksumReport(ctypes.Structure):
     _fields_ = [
         ("checksum_lo", ctypes.c_uint64),
@@ -93,6 +111,20 @@ SIGNATURES = [
     ("rb_debug_speed_clamp", _I32, [_I32, _P, _P, _P, _P, ctypes.c_int64]),
     ("rb_profile_enable", _I32, [_P, _I32]),
     ("rb_profile_take", _I32, [_P, ctypes.POINTER(ctypes.c_double), _PI32]),
+    ("rb_p2p_config_init", None, [ctypes.POINTER(RbP2PConfig)]),
+    ("rb_p2p_create", _I32, [ctypes.POINTER(RbP2PConfig), ctypes.POINTER(_P)]),
+    ("rb_p2p_destroy", None, [_P]),
+    ("rb_p2p_last_error", ctypes.c_char_p, [_P]),
+    ("rb_p2p_set_stream", _I32, [_P, _P]),
+    ("rb_p2p_run_ticks", _I32, [_P, _I32, _P, ctypes.c_int64, _P, _P, _I32]),
+    ("rb_p2p_read_status", _I32, [_P, _P, _P, _P, _P]),
+    ("rb_p2p_read_frames", _I32, [_P, _P, _P]),
+    ("rb_p2p_read_cells", _I32, [_P, _P, _P, _P]),
+    ("rb_p2p_read_live", _I32, [_P, _P]),
+    ("rb_p2p_state_bytes", _I32, [_P]),
+    ("rb_p2p_counters", _I32, [_P, _P]),
+    ("rb_p2p_profile_enable", _I32, [_P, _I32]),
+    ("rb_p2p_profile_take", _I32, [_P, ctypes.POINTER(ctypes.c_double), _PI32]),
 ]
 
 _lib = None

@@ -51,17 +51,6 @@ __global__ void clamp_kernel(const float* __restrict__ vx, const float* __restri
   oy[i] = b;
 }
 
-inline std::unique_ptr<GameOps> make_game(int game, int players, bool lane_per_session) {
-  switch (game) {
-    case RB_GAME_EX_GAME: return make_exgame_ops(players, lane_per_session);
-    case RB_GAME_BRAWLER: return make_brawler_ops(players);
-    case RB_GAME_STUB:
-    case RB_GAME_STUB_ENUM:
-    case RB_GAME_STUB_RANDOM_CS: return make_stub_ops(game, players);
-    default: return nullptr;
-  }
-}
-
 }  // namespace rb
 
 using namespace rb;

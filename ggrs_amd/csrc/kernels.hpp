@@ -519,6 +519,10 @@ __global__ void report_kernel(const typename G::CS* __restrict__ cs, const int32
   out[s] = r;
 }
 
+}  // namespace rb
+#include "p2p.hpp"  // P2PSession kernel (uses load_words / store_words above)
+namespace rb {
+
 struct GameOps {
   virtual ~GameOps() = default;
   int nw = 0, lanes = 1, players = 0, input_bytes = 0, inrec_bytes = 0, cs_bytes = 0, image_bytes = 0, canon_words = 0;
@@ -533,6 +537,8 @@ struct GameOps {
   bool launch_steady_supported(int cd) const { return cd >= 1 && cd <= 8; }
   virtual hipError_t launch_report(const void* cs, const int32_t* err, int S, int32_t frame, void* out,
                                    hipStream_t st) const = 0;
+  // P2PSession ticks (p2p.hpp)
+  virtual hipError_t launch_p2p(const P2PParams& p, int block, hipStream_t st) const = 0;
 };
 
 template <class G>
@@ -596,6 +602,11 @@ struct GameOpsT final : GameOps {
                        reinterpret_cast<rb_checksum_report*>(out));
     return hipGetLastError();
   }
+  hipError_t launch_p2p(const P2PParams& p, int block, hipStream_t st) const override {
+    const int grid = (p.Spad * G::kLanes + block - 1) / block;
+    hipLaunchKernelGGL(p2p_kernel<G>, dim3(grid), dim3(block), 0, st, p);
+    return hipGetLastError();
+  }
 };
 
 
@@ -603,5 +614,16 @@ struct GameOpsT final : GameOps {
 std::unique_ptr<GameOps> make_exgame_ops(int players, bool lane_per_session);
 std::unique_ptr<GameOps> make_brawler_ops(int players);
 std::unique_ptr<GameOps> make_stub_ops(int game, int players);
+
+inline std::unique_ptr<GameOps> make_game(int game, int players, bool lane_per_session) {
+  switch (game) {
+    case RB_GAME_EX_GAME: return make_exgame_ops(players, lane_per_session);
+    case RB_GAME_BRAWLER: return make_brawler_ops(players);
+    case RB_GAME_STUB:
+    case RB_GAME_STUB_ENUM:
+    case RB_GAME_STUB_RANDOM_CS: return make_stub_ops(game, players);
+    default: return nullptr;
+  }
+}
 
 }  // namespace rb

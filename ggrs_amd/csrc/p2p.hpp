@@ -1,0 +1,381 @@
+// ggrs_amd/csrc/p2p.hpp — device side of batched P2PSession rollback
+// (sessions/p2p_session.rs:253-337, 621-673, 778-802 over sync_layer.rs and
+// input_queue.rs), without the network layer.
+//
+// S independent P2P sessions, each seen from one peer: handles in
+// `local_mask` are PlayerType::Local (input delay applies), the others are
+// PlayerType::Remote.  UdpProtocol's only job on this path is to turn packets
+// into Event::Input{input, player} in frame order (p2p_session.rs:838-852);
+// here the caller hands the engine, per tick and remote handle, the newest
+// delivered frame (`upto`) plus the inputs by frame — the device input tensor
+// a batched packet decoder would fill.
+//
+// Unlike SyncTest, P2P bookkeeping is data dependent: a remote input that
+// differs from its prediction sets the InputQueue's first_incorrect_frame, and
+// the next advance_frame rolls back to it (per session).  So the whole
+// request-stream state machine runs on the device, one lane group per session:
+// with one lane per player (ex_game) each lane owns its player's InputQueue
+// (the input_queue.rs state lives in that lane's registers) and the session
+// values (confirmed frame, first incorrect frame) are lane-group minima (DPP).
+// The game state stays in registers across the fused ticks of a launch; every
+// SaveGameState stores the cell (SoA planes), its checksum and its frame tag.
+//
+// Device layout (Spad = S rounded up to 64; L lanes per session):
+//   snap  [W][NW planes][Spad*L]  cells, slot = frame % W (sync_layer.rs:71-75)
+//   cs    [W][Spad] CS            GameStateCell::checksum
+//   tag   [W][Spad] i32           GameStateCell::frame (per session: sessions drift apart)
+//   ring  [128][P][Spad] Input    InputQueue::inputs, slot = frame % 128
+//   live  [NW planes][Spad*L]     game state between launches
+//   qs    [kQsFields][Spad] i32   session + per-player queue scalars (QS_* below)
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "games.hpp"
+
+namespace rb {
+
+// Per-session scalar rows of P2PParams::qs.
+enum : int {
+  QS_CUR = 0,         // SyncLayer::current_frame
+  QS_LAST_SAVED = 1,  // SyncLayer::last_saved_frame
+  QS_LAST_CONF = 2,   // SyncLayer::last_confirmed_frame
+  QS_PLAYER0 = 3,     // + field * 4 + player (4 player slots)
+};
+enum : int {
+  QF_LAST_ADDED = 0,   // InputQueue::last_added_frame
+  QF_PRED_FRAME = 1,   // InputQueue::prediction.frame
+  QF_PRED_VAL = 2,     // InputQueue::prediction.input
+  QF_FIRST_INC = 3,    // InputQueue::first_incorrect_frame
+  QF_LAST_REQ = 4,     // InputQueue::last_requested_frame
+  QF_CONN_LAST = 5,    // ConnectionStatus::last_frame (messages.rs:5-18)
+  QF_COUNT = 6,
+};
+constexpr int kQsFields = QS_PLAYER0 + QF_COUNT * 4;
+// trace rows (the last tick of the last launch): LoadGameState frame, AdvanceFrame count, SaveGameState count
+enum : int { TR_LOAD = 0, TR_NADV = 1, TR_NSAVE = 2, TR_COUNT = 3 };
+constexpr int32_t kP2PStatusOk = 0, kP2PStatusThreshold = 1, kP2PStatusPanic = 101;
+
+struct P2PParams {
+  uint32_t* snap;
+  void* cs;
+  int32_t* tag;
+  void* ring;
+  uint32_t* live;
+  int32_t* qs;
+  int32_t* status;          // [Spad] rb_status of the session's last advance_frame
+  int32_t* trace;           // [TR_COUNT][Spad]
+  uint32_t* counters;       // [0] threshold hits, [1] unexpected-path count, [2] panics
+  const uint8_t* local_in;  // tick t, handle h: local_in + t * local_stride + (h * S + s) * IB
+  int64_t local_stride;
+  const int32_t* upto;      // tick t, handle h: upto[t * upto_stride + h * S + s]
+  int64_t upto_stride;
+  const uint8_t* remote_in;  // frame f, handle h: remote_in + ((f * P + h) * S + s) * IB
+  int32_t remote_frames;
+  int32_t S, Spad, W, delay, remote_delay, T;
+  uint32_t local_mask;
+  int32_t sparse;
+};
+
+// Lane-group reductions over groups of L consecutive lanes (1, 2, 4 or 64).
+template <int L>
+__device__ __forceinline__ int32_t group_min(int32_t v) {
+  if constexpr (L == 64) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v = min(v, __shfl_xor(v, m, 64));
+  } else {
+    if constexpr (L >= 2) v = min(v, __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false));  // [1,0,3,2]
+    if constexpr (L >= 4) v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false));  // [2,3,0,1]
+  }
+  return v;
+}
+
+// One InputQueue (input_queue.rs) in registers, minus the tail/length
+// bookkeeping, which only feeds asserts on valid runs: a frame is confirmed iff
+// it is <= last_added_frame.  The inputs live in the HBM ring.
+struct DevQueue {
+  int32_t last_added, pred_frame, first_inc, last_req, conn_last;
+  uint32_t pred_val;
+};
+
+template <int IB>
+struct RingIO {
+  uint8_t* ring;
+  int P, Spad;
+  __device__ uint32_t get(int32_t f, int h, unsigned s) const {
+    const size_t i = (static_cast<size_t>(f & (kQueueLen - 1)) * P + h) * Spad + s;
+    if constexpr (IB == 4) return reinterpret_cast<const uint32_t*>(ring)[i];
+    else return ring[i];
+  }
+  __device__ void put(int32_t f, int h, unsigned s, uint32_t v) const {
+    const size_t i = (static_cast<size_t>(f & (kQueueLen - 1)) * P + h) * Spad + s;
+    if constexpr (IB == 4) reinterpret_cast<uint32_t*>(ring)[i] = v;
+    else ring[i] = static_cast<uint8_t>(v);
+  }
+};
+
+// input_queue.rs:167-204 add_input_by_frame
+template <int IB>
+__device__ __forceinline__ void q_add_by_frame(DevQueue& q, const RingIO<IB>& r, int h, unsigned s, int32_t f, uint32_t v) {
+  r.put(f, h, s, v);
+  q.last_added = f;
+  if (q.pred_frame != kNullFrame) {
+    if (q.first_inc == kNullFrame && v != q.pred_val) q.first_inc = f;
+    if (q.pred_frame == q.last_req && q.first_inc == kNullFrame) q.pred_frame = kNullFrame;
+    else q.pred_frame += 1;
+  }
+}
+// input_queue.rs:149-163 + 207-239 add_input with the delay already applied to
+// `f`: replicate the entry before head (blank before the first add) up to f.
+template <int IB>
+__device__ __forceinline__ int32_t q_add(DevQueue& q, const RingIO<IB>& r, int h, unsigned s, int32_t f, uint32_t v) {
+  int32_t expected = q.last_added == kNullFrame ? 0 : q.last_added + 1;
+  if (expected > f) return kNullFrame;
+  const uint32_t rep = q.last_added == kNullFrame ? 0u : r.get(q.last_added, h, s);
+  for (; expected < f; ++expected) q_add_by_frame(q, r, h, s, expected, rep);
+  q_add_by_frame(q, r, h, s, f, v);
+  return f;
+}
+// input_queue.rs:104-146 input(requested_frame)
+template <int IB>
+__device__ __forceinline__ uint32_t q_input(DevQueue& q, const RingIO<IB>& r, int h, unsigned s, int32_t f) {
+  q.last_req = f;
+  if (q.pred_frame < 0) {
+    if (q.last_added != kNullFrame && f <= q.last_added) return r.get(f, h, s);  // Confirmed
+    if (f == 0 || q.last_added == kNullFrame) {
+      q.pred_val = 0u;  // blank_input
+      q.pred_frame = 0;  // NULL_FRAME + 1
+    } else {
+      q.pred_val = r.get(q.last_added, h, s);
+      q.pred_frame = q.last_added + 1;
+    }
+  }
+  return q.pred_val;  // Predicted
+}
+
+template <class G>
+__global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
+  using InRec = typename G::InRec;
+  using CS = typename G::CS;
+  constexpr int NW = G::NWL;
+  constexpr int L = G::kLanes;
+  constexpr int P = G::kPlayers, IB = G::kInputBytes;
+  constexpr bool kSplit = L > 1;  // lane h of the group owns player h
+  constexpr int PPL = kSplit ? 1 : P;
+  const unsigned g = blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned s = g / L;
+  const int lane = static_cast<int>(g % L);
+  const bool lead = lane == 0;
+  if (s >= static_cast<unsigned>(p.S)) return;  // whole lane groups leave together
+  const unsigned Spad = static_cast<unsigned>(p.Spad), Gpad = Spad * L;
+  const unsigned slot_words = static_cast<unsigned>(NW) * Gpad;
+  const int W = p.W;
+  CS* __restrict__ csa = reinterpret_cast<CS*>(p.cs);
+  const RingIO<IB> ring{reinterpret_cast<uint8_t*>(p.ring), P, p.Spad};
+  auto qrow = [&](int field, int h) { return p.qs + static_cast<size_t>(QS_PLAYER0 + field * 4 + h) * Spad + s; };
+  auto player_of = [&](int j) { return kSplit ? lane : j; };
+
+  int32_t cur = p.qs[QS_CUR * Spad + s];
+  int32_t last_saved = p.qs[QS_LAST_SAVED * Spad + s];
+  int32_t last_conf = p.qs[QS_LAST_CONF * Spad + s];
+  DevQueue q[PPL];
+#pragma unroll
+  for (int j = 0; j < PPL; ++j) {
+    const int h = player_of(j);
+    if (h < P) {
+      q[j].last_added = *qrow(QF_LAST_ADDED, h);
+      q[j].pred_frame = *qrow(QF_PRED_FRAME, h);
+      q[j].pred_val = static_cast<uint32_t>(*qrow(QF_PRED_VAL, h));
+      q[j].first_inc = *qrow(QF_FIRST_INC, h);
+      q[j].last_req = *qrow(QF_LAST_REQ, h);
+      q[j].conn_last = *qrow(QF_CONN_LAST, h);
+    } else {  // padding lane of a 4-lane group (P = 3): no player
+      q[j] = DevQueue{kNullFrame, kNullFrame, kNullFrame, kNullFrame, INT32_MAX, 0u};
+    }
+  }
+  uint32_t w[NW];
+  load_words<NW>(p.live, static_cast<int>(Gpad), static_cast<int>(g), w);
+
+  int32_t status = kP2PStatusOk, load_frame = kNullFrame, nadv = 0, nsave = 0;
+  uint32_t nonce = 0;
+  // exec = false: bookkeeping only.  When advance_frame returns
+  // Err(PredictionThreshold) the reference drops the request Vec it built
+  // (p2p_session.rs:320 `?`): the sync layer has rolled back, saved and
+  // re-predicted, but the game never loads, saves or advances.  A dry run
+  // reproduces that bookkeeping without touching the game state or the cells.
+  bool exec = true;
+  // SaveGameState{cell, frame}: game checksum, cell.save (sync_layer.rs:118-125)
+  auto save = [&](int32_t f) {
+    last_saved = f;
+    ++nsave;
+    if (!exec) return;
+    CsCtx ctx{0ull, s, nonce++};
+    const CS c = G::checksum(w, f, lane, ctx);
+    const unsigned slot = static_cast<unsigned>(f % W);
+    store_words<NW>(p.snap + slot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), w);
+    if (lead) {
+      csa[slot * Spad + s] = c;
+      p.tag[slot * Spad + s] = f;
+    }
+  };
+  // SyncLayer::synchronized_inputs (sync_layer.rs:187-200) for this lane's players
+  auto sync_inputs = [&](int32_t f) -> InRec {
+    uint64_t rec = 0;
+#pragma unroll
+    for (int j = 0; j < PPL; ++j) {
+      const int h = player_of(j);
+      if (h < P) rec |= static_cast<uint64_t>(q_input<IB>(q[j], ring, h, s, f)) << (8 * IB * h);
+    }
+    return static_cast<InRec>(rec);
+  };
+  auto advance = [&](int32_t f) {  // AdvanceFrame{inputs}
+    const InRec rec = sync_inputs(f);
+    ++nadv;
+    if (exec) G::advance(w, rec, lane, 0u, &p.counters[1]);
+  };
+  // P2PSession::adjust_gamestate (p2p_session.rs:621-673)
+  auto adjust = [&](int32_t first_incorrect, int32_t min_confirmed) {
+    const int32_t to_load = p.sparse ? last_saved : first_incorrect;
+    const int32_t count = cur - to_load;
+    const unsigned slot = static_cast<unsigned>(to_load % W);
+    if (to_load < 0 || to_load > first_incorrect || count > W || p.tag[slot * Spad + s] != to_load) {
+      status = kP2PStatusPanic;  // a reference assert (sync_layer.rs:141-148) would fire
+      return;
+    }
+    if (exec) load_words<NW>(p.snap + slot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), w);  // LoadGameState
+    load_frame = to_load;
+    cur = to_load;
+#pragma unroll
+    for (int j = 0; j < PPL; ++j) {  // SyncLayer::reset_prediction
+      q[j].pred_frame = kNullFrame;
+      q[j].first_inc = kNullFrame;
+      q[j].last_req = kNullFrame;
+    }
+    for (int32_t i = 0; i < count; ++i) {
+      if (p.sparse ? cur == min_confirmed : i > 0) save(cur);
+      advance(cur);
+      cur += 1;
+    }
+  };
+  // advance_frame (p2p_session.rs:253-303) up to the local inputs: frame-0
+  // save, rollback, save / sparse check, set_last_confirmed_frame.
+  auto rollback_and_save = [&]() {
+    load_frame = kNullFrame;
+    nadv = nsave = 0;
+    if (cur == 0) save(cur);
+    int32_t confirmed = INT32_MAX, first_inc = INT32_MAX;
+#pragma unroll
+    for (int j = 0; j < PPL; ++j) {
+      confirmed = min(confirmed, q[j].conn_last);  // confirmed_frame (:487-498)
+      if (q[j].first_inc != kNullFrame) first_inc = min(first_inc, q[j].first_inc);  // check_simulation_consistency
+    }
+    confirmed = group_min<L>(confirmed);
+    first_inc = group_min<L>(first_inc);
+    if (first_inc != INT32_MAX) adjust(first_inc, confirmed);
+    if (status == kP2PStatusPanic) return;
+    if (p.sparse) {  // check_last_saved_state (:778-802)
+      if (cur - last_saved >= W) {
+        if (confirmed >= cur) save(cur);
+        else adjust(last_saved, confirmed);
+      }
+    } else {
+      save(cur);
+    }
+    last_conf = p.sparse ? min(confirmed, last_saved) : confirmed;  // set_last_confirmed_frame (sync_layer.rs:220-244)
+  };
+
+  for (int t = 0; t < p.T; ++t) {
+    status = kP2PStatusOk;
+    // ---- poll_remote_clients: Event::Input in frame order (handle_event, :838-852)
+#pragma unroll
+    for (int j = 0; j < PPL; ++j) {
+      const int h = player_of(j);
+      if (h >= P || ((p.local_mask >> h) & 1u)) continue;
+      const int32_t up = p.upto[static_cast<int64_t>(t) * p.upto_stride + static_cast<int64_t>(h) * p.S + s];
+      int32_t f = q[j].conn_last == kNullFrame ? p.remote_delay : q[j].conn_last + 1;
+      for (; f <= up && f < p.remote_frames; ++f) {
+        const uint8_t* src = p.remote_in + (static_cast<size_t>(f) * P + h) * p.S * IB + static_cast<size_t>(s) * IB;
+        const uint32_t v = IB == 4 ? *reinterpret_cast<const uint32_t*>(src) : *src;
+        q_add<IB>(q[j], ring, h, s, f, v);  // add_remote_input (frame delay 0)
+        q[j].conn_last = f;
+      }
+    }
+    // ---- PredictionThreshold (sync_layer.rs:163-167) is decided by bookkeeping
+    // alone: without sparse saving from the confirmed frame, with it by a dry run.
+    bool threshold;
+    if (!p.sparse) {
+      int32_t confirmed = INT32_MAX;
+#pragma unroll
+      for (int j = 0; j < PPL; ++j) confirmed = min(confirmed, q[j].conn_last);
+      confirmed = group_min<L>(confirmed);
+      threshold = cur >= W && cur - confirmed >= W;
+      if (threshold) {
+        exec = false;
+        rollback_and_save();
+        exec = true;
+      }
+    } else {
+      const int32_t cur0 = cur, ls0 = last_saved;
+      DevQueue q0[PPL];
+#pragma unroll
+      for (int j = 0; j < PPL; ++j) q0[j] = q[j];
+      exec = false;
+      rollback_and_save();
+      exec = true;
+      threshold = status != kP2PStatusPanic && cur >= W && cur - last_conf >= W;
+      if (!threshold && status != kP2PStatusPanic) {
+        cur = cur0;
+        last_saved = ls0;
+#pragma unroll
+        for (int j = 0; j < PPL; ++j) q[j] = q0[j];
+      }
+    }
+    if (status == kP2PStatusPanic) break;
+    if (threshold) {
+      status = kP2PStatusThreshold;  // Err(PredictionThreshold): the game does not move this tick
+      load_frame = kNullFrame;       // and the user never sees the dropped requests
+      nadv = nsave = 0;
+      if (lead) atomicAdd(&p.counters[0], 1u);
+      continue;
+    }
+    rollback_and_save();
+    if (status == kP2PStatusPanic) break;
+    // ---- local inputs: SyncLayer::add_local_input (sync_layer.rs:159-174)
+#pragma unroll
+    for (int j = 0; j < PPL; ++j) {
+      const int h = player_of(j);
+      if (h >= P || !((p.local_mask >> h) & 1u)) continue;
+      const uint8_t* src = p.local_in + static_cast<int64_t>(t) * p.local_stride +
+                           (static_cast<size_t>(h) * p.S + s) * IB;
+      const uint32_t v = IB == 4 ? *reinterpret_cast<const uint32_t*>(src) : *src;
+      q[j].conn_last = q_add<IB>(q[j], ring, h, s, cur + p.delay, v);  // local_connect_status[h].last_frame
+    }
+    advance(cur);
+    cur += 1;
+  }
+
+  // ---- write back
+  store_words<NW>(p.live, static_cast<int>(Gpad), static_cast<int>(g), w);
+#pragma unroll
+  for (int j = 0; j < PPL; ++j) {
+    const int h = player_of(j);
+    if (h >= P) continue;
+    *qrow(QF_LAST_ADDED, h) = q[j].last_added;
+    *qrow(QF_PRED_FRAME, h) = q[j].pred_frame;
+    *qrow(QF_PRED_VAL, h) = static_cast<int32_t>(q[j].pred_val);
+    *qrow(QF_FIRST_INC, h) = q[j].first_inc;
+    *qrow(QF_LAST_REQ, h) = q[j].last_req;
+    *qrow(QF_CONN_LAST, h) = q[j].conn_last;
+  }
+  if (lead) {
+    p.qs[QS_CUR * Spad + s] = cur;
+    p.qs[QS_LAST_SAVED * Spad + s] = last_saved;
+    p.qs[QS_LAST_CONF * Spad + s] = last_conf;
+    p.status[s] = status;
+    p.trace[TR_LOAD * Spad + s] = load_frame;
+    p.trace[TR_NADV * Spad + s] = nadv;
+    p.trace[TR_NSAVE * Spad + s] = nsave;
+    if (status == kP2PStatusPanic) atomicAdd(&p.counters[2], 1u);
+  }
+}
+
+}  // namespace rb

@@ -1,0 +1,340 @@
+// ggrs_amd/csrc/p2p_engine.hip — host side of the P2PSession batches
+// (include/ggrs_amd.h rb_p2p_*): buffers, validation (builder.rs), launches of
+// p2p_kernel (p2p.hpp) and the read-backs the parity tests use.
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "kernels.hpp"
+
+using namespace rb;
+
+struct rb_p2p {
+  rb_p2p_config cfg{};
+  std::unique_ptr<GameOps> ops;
+  int S = 0, Spad = 0, W = 0, P = 0, block = 256;
+  int device = 0;
+  hipStream_t own_stream = nullptr, stream = nullptr;
+  uint32_t* snap = nullptr;
+  void* cs = nullptr;
+  int32_t* tag = nullptr;
+  void* ring = nullptr;
+  uint32_t* live = nullptr;
+  int32_t* qs = nullptr;
+  int32_t* status = nullptr;
+  int32_t* trace = nullptr;
+  uint32_t* counters = nullptr;
+  bool prof = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev;
+  size_t prof_used = 0;
+  std::string last_err;
+};
+
+namespace {
+thread_local std::string g_p2p_err;
+
+rb_status pfail(rb_p2p* b, rb_status st, const std::string& msg) {
+  if (b) b->last_err = msg;
+  else g_p2p_err = msg;
+  return st;
+}
+#define P2P_TRY(b, expr)                                                                                    \
+  do {                                                                                                      \
+    hipError_t _e = (expr);                                                                                 \
+    if (_e != hipSuccess) return pfail((b), RB_DEVICE_ERROR, std::string(#expr ": ") + hipGetErrorString(_e)); \
+  } while (0)
+
+void free_all(rb_p2p* b) {
+  (void)hipSetDevice(b->device);
+  if (b->stream) (void)hipStreamSynchronize(b->stream);
+  void* ptrs[] = {b->snap, b->cs, b->tag, b->ring, b->live, b->qs, b->status, b->trace, b->counters};
+  for (void* q : ptrs)
+    if (q) (void)hipFree(q);
+  for (auto& pr : b->prof_ev) {
+    (void)hipEventDestroy(pr.first);
+    (void)hipEventDestroy(pr.second);
+  }
+  if (b->own_stream) (void)hipStreamDestroy(b->own_stream);
+}
+
+template <class T>
+rb_status read_rows(rb_p2p* b, const T* dev, size_t rows, std::vector<T>& host) {
+  host.resize(rows * static_cast<size_t>(b->Spad));
+  P2P_TRY(b, hipMemcpyAsync(host.data(), dev, host.size() * sizeof(T), hipMemcpyDeviceToHost, b->stream));
+  P2P_TRY(b, hipStreamSynchronize(b->stream));
+  return RB_OK;
+}
+
+// session s's words [lanes][nw] from a block of lane planes, as its canonical image
+void image_from_planes(const rb_p2p* b, const std::vector<uint32_t>& planes, int s, int32_t frame, uint8_t* out) {
+  const int L = b->ops->lanes, NW = b->ops->nw;
+  std::vector<uint32_t> w(static_cast<size_t>(L) * NW);
+  for (int l = 0; l < L; ++l)
+    for (int k = 0; k < NW; ++k) w[l * NW + k] = planes[word_index(NW, b->Spad * L, s * L + l, k)];
+  b->ops->image(w.data(), frame, out);
+}
+}  // namespace
+
+extern "C" {
+
+void rb_p2p_config_init(rb_p2p_config* c) {
+  std::memset(c, 0, sizeof(*c));
+  c->abi_version = RB_ABI_VERSION;
+  c->game = RB_GAME_EX_GAME;
+  c->num_sessions = 1;
+  c->num_players = 2;     // builder.rs:13
+  c->max_prediction = 8;  // builder.rs:20
+  c->input_delay = 0;     // builder.rs:16
+  c->device = 0;
+  c->local_mask = 1u;     // handle 0 local, handle 1 remote (ex_game_p2p.rs's two-peer setup)
+  c->remote_delay = 0;
+  c->sparse_saving = 0;   // builder.rs:17 DEFAULT_SAVE_MODE
+}
+
+const char* rb_p2p_last_error(const rb_p2p* b) { return b ? b->last_err.c_str() : g_p2p_err.c_str(); }
+
+rb_status rb_p2p_create(const rb_p2p_config* cfg, rb_p2p** out) {
+  *out = nullptr;
+  if (!cfg || cfg->abi_version != RB_ABI_VERSION) return pfail(nullptr, RB_INVALID_REQUEST, "rb_p2p_config.abi_version mismatch");
+  if (cfg->max_prediction <= 0)  // builder.rs:136-145
+    return pfail(nullptr, RB_INVALID_REQUEST, "Currently, only prediction windows above 0 are supported");
+  if (cfg->num_players <= 0 || cfg->num_players > 4 || cfg->num_sessions <= 0 || cfg->input_delay < 0 ||
+      cfg->remote_delay < 0)
+    return pfail(nullptr, RB_INVALID_REQUEST, "num_players must be 1..4; sizes and delays non-negative");
+  const uint32_t all = (1u << cfg->num_players) - 1u;
+  if ((cfg->local_mask & ~all) != 0)  // builder.rs:103-115: handles must be < num_players
+    return pfail(nullptr, RB_INVALID_REQUEST,
+                 "The player handle you provided is invalid. For a local player, the handle should be between 0 and num_players");
+  if (cfg->local_mask == 0 || cfg->local_mask == all)
+    return pfail(nullptr, RB_INVALID_REQUEST, "a P2P batch needs at least one local and one remote handle");
+  if (cfg->max_prediction > 64 || cfg->input_delay + cfg->max_prediction + 2 > kQueueLen)
+    return pfail(nullptr, RB_INVALID_REQUEST, "max_prediction / input delay do not fit the 128-entry input queue");
+  if (cfg->game != RB_GAME_EX_GAME && cfg->game != RB_GAME_STUB && cfg->game != RB_GAME_BRAWLER)
+    return pfail(nullptr, RB_INVALID_REQUEST, "P2P batches support ex_game, the stub game and the brawler");
+  auto ops = make_game(cfg->game, cfg->num_players, (cfg->flags & RB_FLAG_LANE_PER_SESSION) != 0);
+  if (!ops) return pfail(nullptr, RB_INVALID_REQUEST, "unsupported game / num_players combination");
+  if (static_cast<uint64_t>(cfg->max_prediction) * ops->nw * ops->lanes *
+          ((static_cast<uint64_t>(cfg->num_sessions) + 63) / 64 * 64) >= (1ull << 32))
+    return pfail(nullptr, RB_INVALID_REQUEST, "batch too large for 32-bit snapshot offsets");
+
+  auto b = std::make_unique<rb_p2p>();
+  b->cfg = *cfg;
+  b->ops = std::move(ops);
+  b->S = cfg->num_sessions;
+  b->Spad = (cfg->num_sessions + 63) / 64 * 64;
+  b->W = cfg->max_prediction;
+  b->P = cfg->num_players;
+  b->block = cfg->block_size ? static_cast<int>(cfg->block_size) : 256;
+  if (b->block % 64 != 0 || b->block > 256) return pfail(nullptr, RB_INVALID_REQUEST, "block_size must be 64, 128, 192 or 256");
+  b->device = cfg->device;
+  rb_p2p* bp = b.get();
+  auto hip_fail = [&](hipError_t e, const char* what) {
+    g_p2p_err = std::string(what) + ": " + hipGetErrorString(e);
+    free_all(bp);
+    return RB_DEVICE_ERROR;
+  };
+#define P2P_CREATE(expr)                              \
+  do {                                                \
+    hipError_t _e = (expr);                           \
+    if (_e != hipSuccess) return hip_fail(_e, #expr); \
+  } while (0)
+  P2P_CREATE(hipSetDevice(b->device));
+  P2P_CREATE(hipStreamCreateWithFlags(&b->own_stream, hipStreamNonBlocking));
+  b->stream = b->own_stream;
+  const size_t Sp = b->Spad, NW = b->ops->nw, W = b->W, L = b->ops->lanes, Gp = Sp * L;
+  const size_t ring_bytes = static_cast<size_t>(kQueueLen) * b->P * Sp * b->ops->input_bytes;
+  P2P_CREATE(hipMalloc(&b->snap, W * NW * Gp * 4));
+  P2P_CREATE(hipMalloc(&b->cs, W * Sp * b->ops->cs_bytes));
+  P2P_CREATE(hipMalloc(&b->tag, W * Sp * 4));
+  P2P_CREATE(hipMalloc(&b->ring, ring_bytes));
+  P2P_CREATE(hipMalloc(&b->live, NW * Gp * 4));
+  P2P_CREATE(hipMalloc(&b->qs, kQsFields * Sp * 4));
+  P2P_CREATE(hipMalloc(&b->status, Sp * 4));
+  P2P_CREATE(hipMalloc(&b->trace, TR_COUNT * Sp * 4));
+  P2P_CREATE(hipMalloc(&b->counters, 16));
+  P2P_CREATE(hipMemsetAsync(b->snap, 0, W * NW * Gp * 4, b->stream));
+  P2P_CREATE(hipMemsetAsync(b->cs, 0, W * Sp * b->ops->cs_bytes, b->stream));
+  P2P_CREATE(hipMemsetAsync(b->tag, 0xff, W * Sp * 4, b->stream));  // GameState::default frame = NULL_FRAME
+  P2P_CREATE(hipMemsetAsync(b->ring, 0, ring_bytes, b->stream));     // blank inputs
+  P2P_CREATE(hipMemsetAsync(b->status, 0, Sp * 4, b->stream));
+  P2P_CREATE(hipMemsetAsync(b->trace, 0xff, TR_COUNT * Sp * 4, b->stream));
+  P2P_CREATE(hipMemsetAsync(b->counters, 0, 16, b->stream));
+  // SyncLayer::new / InputQueue::new / ConnectionStatus::default: every frame NULL, current 0
+  std::vector<int32_t> qs(kQsFields * Sp, kNullFrame);
+  for (size_t s = 0; s < Sp; ++s) {
+    qs[QS_CUR * Sp + s] = 0;
+    for (int h = 0; h < 4; ++h) qs[(QS_PLAYER0 + QF_PRED_VAL * 4 + h) * Sp + s] = 0;
+  }
+  P2P_CREATE(hipMemcpyAsync(b->qs, qs.data(), qs.size() * 4, hipMemcpyHostToDevice, b->stream));
+  // State::new for every session
+  std::vector<uint32_t> w0(L * NW), planes(NW * Gp);
+  b->ops->init_words(w0.data());
+  for (size_t s = 0; s < Sp; ++s)
+    for (size_t l = 0; l < L; ++l)
+      for (size_t k = 0; k < NW; ++k)
+        planes[word_index(static_cast<int>(NW), static_cast<int>(Gp), static_cast<int>(s * L + l), static_cast<int>(k))] =
+            w0[l * NW + k];
+  P2P_CREATE(hipMemcpyAsync(b->live, planes.data(), planes.size() * 4, hipMemcpyHostToDevice, b->stream));
+  P2P_CREATE(hipStreamSynchronize(b->stream));
+#undef P2P_CREATE
+  *out = b.release();
+  return RB_OK;
+}
+
+void rb_p2p_destroy(rb_p2p* b) {
+  if (!b) return;
+  free_all(b);
+  delete b;
+}
+
+rb_status rb_p2p_set_stream(rb_p2p* b, void* s) {
+  P2P_TRY(b, hipStreamSynchronize(b->stream));
+  b->stream = s ? static_cast<hipStream_t>(s) : b->own_stream;
+  return RB_OK;
+}
+
+int32_t rb_p2p_state_bytes(const rb_p2p* b) { return b->ops->image_bytes; }
+
+rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs, int64_t local_stride,
+                           const int32_t* remote_upto, const void* remote_inputs, int32_t remote_frames) {
+  if (n_ticks <= 0) return RB_OK;
+  if (!local_inputs || !remote_upto || !remote_inputs || remote_frames <= 0)
+    return pfail(b, RB_INVALID_REQUEST, "rb_p2p_run_ticks: missing input tensor");
+  P2PParams p{};
+  p.snap = b->snap;
+  p.cs = b->cs;
+  p.tag = b->tag;
+  p.ring = b->ring;
+  p.live = b->live;
+  p.qs = b->qs;
+  p.status = b->status;
+  p.trace = b->trace;
+  p.counters = b->counters;
+  p.local_in = static_cast<const uint8_t*>(local_inputs);
+  p.local_stride = local_stride;
+  p.upto = remote_upto;
+  p.upto_stride = static_cast<int64_t>(b->P) * b->S;
+  p.remote_in = static_cast<const uint8_t*>(remote_inputs);
+  p.remote_frames = remote_frames;
+  p.S = b->S;
+  p.Spad = b->Spad;
+  p.W = b->W;
+  p.delay = b->cfg.input_delay;
+  p.remote_delay = b->cfg.remote_delay;
+  p.T = n_ticks;
+  p.local_mask = b->cfg.local_mask;
+  p.sparse = b->cfg.sparse_saving != 0;
+  P2P_TRY(b, hipSetDevice(b->device));
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (b->prof) {
+    if (b->prof_used == b->prof_ev.size()) {
+      P2P_TRY(b, hipEventCreate(&e0));
+      P2P_TRY(b, hipEventCreate(&e1));
+      b->prof_ev.emplace_back(e0, e1);
+    }
+    e0 = b->prof_ev[b->prof_used].first;
+    e1 = b->prof_ev[b->prof_used].second;
+    ++b->prof_used;
+    P2P_TRY(b, hipEventRecord(e0, b->stream));
+  }
+  hipError_t e = b->ops->launch_p2p(p, b->block, b->stream);
+  if (e != hipSuccess) return pfail(b, RB_DEVICE_ERROR, std::string("p2p launch: ") + hipGetErrorString(e));
+  if (b->prof) P2P_TRY(b, hipEventRecord(e1, b->stream));
+  return RB_OK;
+}
+
+rb_status rb_p2p_read_status(rb_p2p* b, int32_t* status, int32_t* load_frame, int32_t* n_adv, int32_t* n_save) {
+  std::vector<int32_t> st, tr;
+  rb_status r = read_rows(b, b->status, 1, st);
+  if (r == RB_OK) r = read_rows(b, b->trace, TR_COUNT, tr);
+  if (r != RB_OK) return r;
+  const size_t Sp = b->Spad;
+  for (int s = 0; s < b->S; ++s) {
+    if (status) status[s] = st[s] == kP2PStatusPanic ? RB_PANIC : st[s];
+    if (load_frame) load_frame[s] = tr[TR_LOAD * Sp + s];
+    if (n_adv) n_adv[s] = tr[TR_NADV * Sp + s];
+    if (n_save) n_save[s] = tr[TR_NSAVE * Sp + s];
+  }
+  return RB_OK;
+}
+
+rb_status rb_p2p_read_frames(rb_p2p* b, int32_t* current, int32_t* confirmed) {
+  std::vector<int32_t> qs;
+  rb_status r = read_rows(b, b->qs, kQsFields, qs);
+  if (r != RB_OK) return r;
+  for (int s = 0; s < b->S; ++s) {
+    if (current) current[s] = qs[QS_CUR * b->Spad + s];
+    if (confirmed) confirmed[s] = qs[QS_LAST_CONF * b->Spad + s];
+  }
+  return RB_OK;
+}
+
+rb_status rb_p2p_read_cells(rb_p2p* b, int32_t* tags, void* images, uint64_t* checksums) {
+  std::vector<int32_t> tg;
+  rb_status r = read_rows(b, b->tag, b->W, tg);
+  if (r != RB_OK) return r;
+  const size_t Sp = b->Spad, L = b->ops->lanes, NW = b->ops->nw, B = b->ops->image_bytes;
+  std::vector<uint8_t> csh(b->W * Sp * b->ops->cs_bytes);
+  P2P_TRY(b, hipMemcpy(csh.data(), b->cs, csh.size(), hipMemcpyDeviceToHost));
+  std::vector<uint32_t> planes;
+  for (int w = 0; w < b->W; ++w) {
+    if (images) {
+      r = read_rows(b, b->snap + static_cast<size_t>(w) * NW * Sp * L, NW * L, planes);
+      if (r != RB_OK) return r;
+    }
+    for (int s = 0; s < b->S; ++s) {
+      const int32_t f = tg[w * Sp + s];
+      if (tags) tags[static_cast<size_t>(w) * b->S + s] = f;
+      if (images) image_from_planes(b, planes, s, f, static_cast<uint8_t*>(images) + (static_cast<size_t>(w) * b->S + s) * B);
+      if (checksums) {
+        const U128 c = b->ops->cs_at(csh.data(), static_cast<size_t>(w) * Sp + s);
+        checksums[(static_cast<size_t>(w) * b->S + s) * 2] = c.lo;
+        checksums[(static_cast<size_t>(w) * b->S + s) * 2 + 1] = c.hi;
+      }
+    }
+  }
+  return RB_OK;
+}
+
+rb_status rb_p2p_read_live(rb_p2p* b, void* images) {
+  std::vector<int32_t> qs;
+  std::vector<uint32_t> planes;
+  rb_status r = read_rows(b, b->qs, kQsFields, qs);
+  if (r == RB_OK) r = read_rows(b, b->live, static_cast<size_t>(b->ops->nw) * b->ops->lanes, planes);
+  if (r != RB_OK) return r;
+  for (int s = 0; s < b->S; ++s)
+    image_from_planes(b, planes, s, qs[QS_CUR * b->Spad + s],
+                      static_cast<uint8_t*>(images) + static_cast<size_t>(s) * b->ops->image_bytes);
+  return RB_OK;
+}
+
+rb_status rb_p2p_counters(rb_p2p* b, uint32_t* out3) {
+  uint32_t c[4];
+  P2P_TRY(b, hipStreamSynchronize(b->stream));
+  P2P_TRY(b, hipMemcpy(c, b->counters, 16, hipMemcpyDeviceToHost));
+  for (int i = 0; i < 3; ++i) out3[i] = c[i];
+  return RB_OK;
+}
+
+rb_status rb_p2p_profile_enable(rb_p2p* b, int32_t on) {
+  b->prof = on != 0;
+  return RB_OK;
+}
+
+rb_status rb_p2p_profile_take(rb_p2p* b, double* total_ms, int32_t* launches) {
+  double t = 0;
+  if (b->prof_used > 0) {
+    P2P_TRY(b, hipEventSynchronize(b->prof_ev[b->prof_used - 1].second));
+    for (size_t i = 0; i < b->prof_used; ++i) {
+      float ms = 0;
+      P2P_TRY(b, hipEventElapsedTime(&ms, b->prof_ev[i].first, b->prof_ev[i].second));
+      t += ms;
+    }
+  }
+  if (total_ms) *total_ms = t;
+  if (launches) *launches = static_cast<int32_t>(b->prof_used);
+  b->prof_used = 0;
+  return RB_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,182 @@
+"""P2PSession batches over the C ABI (include/ggrs_amd.h rb_p2p_*).
+
+Mirrors sessions/p2p_session.rs for ``num_sessions`` independent sessions seen
+from one peer.  The network layer is the caller's: per tick it hands over, for
+every remote handle, the newest delivered frame and the inputs by frame — what
+UdpProtocol's Event::Input stream (p2p_session.rs:838-852) carries.  Built by
+``SessionBuilder.add_player(...).start_p2p_session()`` (builder.rs:251-308).
+
+``synth_network`` produces a deterministic synthetic delivery schedule (per
+session latency + jitter) for tests and the bench.
+"""
+from __future__ import annotations
+
+import ctypes
+import enum
+
+import numpy as np
+
+from . import _lib as L
+from .session import INPUT_DTYPE, DeviceError, Panic
+from .synth import SEED, splitmix64
+
+
+class PlayerType(enum.Enum):  # lib.rs:115-124 (Spectator is not part of the batch)
+    Local = "local"
+    Remote = "remote"
+
+
+def _dev_ptr(x):
+    """(pointer, keepalive) of a torch CUDA tensor."""
+    import torch
+    if not isinstance(x, torch.Tensor) or not x.is_cuda:
+        raise TypeError("P2P tensors must be torch CUDA tensors (device memory, stream ordered)")
+    x = x.contiguous()
+    return ctypes.c_void_p(x.data_ptr()), x
+
+
+class P2PSession:
+    """p2p_session.rs:116-929 (rollback path) for ``num_sessions`` sessions."""
+
+    def __init__(self, lib, handle, game, cfg):
+        self._lib = lib
+        self._h = handle
+        self.game = game
+        self.num_sessions = int(cfg.num_sessions)
+        self.num_players = int(cfg.num_players)
+        self.max_prediction = int(cfg.max_prediction)
+        self.input_delay = int(cfg.input_delay)
+        self.remote_delay = int(cfg.remote_delay)
+        self.sparse_saving = bool(cfg.sparse_saving)
+        self.local_mask = int(cfg.local_mask)
+        self.state_bytes = lib.rb_p2p_state_bytes(handle)
+        self.input_dtype = INPUT_DTYPE[game]
+        self._keep = []
+
+    def close(self):
+        if self._h:
+            self._lib.rb_p2p_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, st):
+        if st != L.RB_OK:
+            msg = (self._lib.rb_p2p_last_error(self._h) or b"").decode()
+            raise DeviceError(msg) if st == L.RB_DEVICE_ERROR else Panic(msg)
+
+    def local_player_handles(self):  # p2p_session.rs:416-419
+        return [h for h in range(self.num_players) if (self.local_mask >> h) & 1]
+
+    def remote_player_handles(self):  # :421-424
+        return [h for h in range(self.num_players) if not (self.local_mask >> h) & 1]
+
+    def set_stream(self, stream) -> None:
+        self._check(self._lib.rb_p2p_set_stream(self._h, ctypes.c_void_p(stream.cuda_stream if stream else 0)))
+
+    def run_ticks(self, local_inputs, remote_upto, remote_inputs) -> None:
+        """T ticks: [poll_remote_clients, add_local_input for every local handle,
+        advance_frame, handle_requests] x T in one device launch.
+
+        local_inputs  [T, P, S] Input values (remote handles' rows ignored)
+        remote_upto   [T, P, S] int32 newest delivered frame per remote handle
+        remote_inputs [F, P, S] Input values by frame (local handles' rows ignored)
+        All torch CUDA tensors on the batch's device."""
+        T = int(local_inputs.shape[0])
+        assert tuple(local_inputs.shape[1:]) == (self.num_players, self.num_sessions)
+        assert tuple(remote_upto.shape) == (T, self.num_players, self.num_sessions)
+        assert tuple(remote_inputs.shape[1:]) == (self.num_players, self.num_sessions)
+        lp, lk = _dev_ptr(local_inputs)
+        up, uk = _dev_ptr(remote_upto)
+        rp, rk = _dev_ptr(remote_inputs)
+        self._keep = [lk, uk, rk]
+        stride = self.num_players * self.num_sessions * lk.element_size()
+        self._check(self._lib.rb_p2p_run_ticks(self._h, T, lp, stride, up, rp, int(remote_inputs.shape[0])))
+
+    def advance_frame(self, local_inputs, remote_upto, remote_inputs) -> None:
+        """One tick (run_ticks with T = 1): local_inputs [P, S], remote_upto [P, S]."""
+        self.run_ticks(local_inputs[None], remote_upto[None], remote_inputs)
+
+    def status(self):
+        """(rb_status [S], LoadGameState frame [S] (NULL_FRAME = no rollback),
+        AdvanceFrame count [S], SaveGameState count [S]) of the last tick."""
+        st, lf, na, ns = (np.empty(self.num_sessions, np.int32) for _ in range(4))
+        p = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+        self._check(self._lib.rb_p2p_read_status(self._h, p(st), p(lf), p(na), p(ns)))
+        return st, lf, na, ns
+
+    def frames(self):
+        """(current_frame [S], last confirmed frame [S])."""
+        c = np.empty(self.num_sessions, np.int32)
+        k = np.empty(self.num_sessions, np.int32)
+        self._check(self._lib.rb_p2p_read_frames(self._h, c.ctypes.data_as(ctypes.c_void_p),
+                                                 k.ctypes.data_as(ctypes.c_void_p)))
+        return c, k
+
+    def read_cells(self):
+        """(frame tags [W, S], images [W, S, B], checksums [W, S, 2])."""
+        W, S = self.max_prediction, self.num_sessions
+        tags = np.empty((W, S), np.int32)
+        img = np.zeros((W, S, self.state_bytes), np.uint8)
+        cs = np.zeros((W, S, 2), np.uint64)
+        self._check(self._lib.rb_p2p_read_cells(self._h, tags.ctypes.data_as(ctypes.c_void_p),
+                                                img.ctypes.data_as(ctypes.c_void_p), cs.ctypes.data_as(ctypes.c_void_p)))
+        return tags, img, cs
+
+    def read_live(self):
+        img = np.zeros((self.num_sessions, self.state_bytes), np.uint8)
+        self._check(self._lib.rb_p2p_read_live(self._h, img.ctypes.data_as(ctypes.c_void_p)))
+        return img
+
+    def counters(self):
+        """(PredictionThreshold hits, unexpected math paths, panicked sessions) since create."""
+        c = (ctypes.c_uint32 * 3)()
+        self._check(self._lib.rb_p2p_counters(self._h, c))
+        return tuple(c)
+
+    def profile_enable(self, on: bool) -> None:
+        self._check(self._lib.rb_p2p_profile_enable(self._h, int(on)))
+
+    def profile_take(self):
+        ms = ctypes.c_double()
+        n = ctypes.c_int32()
+        self._check(self._lib.rb_p2p_profile_take(self._h, ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+
+def synth_network(num_sessions: int, num_players: int, ticks: int, local_mask: int, remote_delay: int,
+                  min_lag: int = 1, max_lag: int = 4, seed: int = SEED, first_session: int = 0,
+                  dtype=np.uint8, mask: int = 0x0F):
+    """A deterministic two-way network of peers in lock-step (numpy).
+
+    Remote handle h's peer adds its local input for its frame f at frame
+    f + remote_delay and sends it; it reaches us ``lag`` ticks later, with lag
+    drawn per (session, tick) in [min_lag, max_lag] by splitmix64.  Deliveries
+    are in order (UdpProtocol's sequencing): remote_upto[t] is the running
+    maximum of (t - 1 - lag + remote_delay).
+
+    Returns (local_inputs [T, P, S], remote_upto int32 [T, P, S],
+    remote_inputs [T + remote_delay, P, S] by frame)."""
+    from .synth import synth_inputs
+    S, P, T = num_sessions, num_players, ticks
+    inputs = synth_inputs(S, P, T, seed=seed, mask=mask, dtype=dtype, first_session=first_session)
+    remote_in = np.zeros((T + remote_delay, P, S), dtype)
+    remote_in[remote_delay:] = inputs  # the peer's input for its frame f lands at frame f + delay
+    s = np.arange(first_session, first_session + S, dtype=np.uint64)[None, :]
+    p = np.arange(P, dtype=np.uint64)[:, None]
+    upto = np.empty((T, P, S), np.int32)
+    run = np.full((P, S), -1, np.int64)
+    span = max_lag - min_lag + 1
+    for t in range(T):
+        h = splitmix64(np.uint64(seed ^ 0x6E6574) ^ ((s << np.uint64(24)) + (p << np.uint64(20)) + np.uint64(t)))
+        lag = min_lag + (h % np.uint64(span)).astype(np.int64)
+        run = np.maximum(run, t - 1 - lag + remote_delay)
+        upto[t] = np.minimum(run, T + remote_delay - 1)
+    for hnd in range(P):
+        if (local_mask >> hnd) & 1:
+            upto[:, hnd] = -1
+    return inputs, upto, remote_in

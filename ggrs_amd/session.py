@@ -213,6 +213,62 @@ class SessionBuilder:
         self._cfg.block_size = int(block)
         return self
 
+    # -- P2P (builder.rs:90-128, 159-166, 251-308)
+    def add_player(self, player_type: "PlayerType", player_handle: int) -> "SessionBuilder":
+        """PlayerType.Local or PlayerType.Remote for handle < num_players.  The
+        remote's address is not needed: the batch takes delivered inputs
+        directly (P2PSession.run_ticks)."""
+        from .p2p import PlayerType
+        players = getattr(self, "_players", {})
+        if player_handle in players:
+            raise InvalidRequest("Player handle already in use.")
+        if player_type not in (PlayerType.Local, PlayerType.Remote):
+            raise InvalidRequest("spectators are not part of the P2P batch")
+        players[int(player_handle)] = player_type
+        self._players = players
+        return self
+
+    def with_sparse_saving_mode(self, sparse_saving: bool) -> "SessionBuilder":  # :159-166
+        self._sparse = bool(sparse_saving)
+        return self
+
+    def with_remote_input_delay(self, delay: int) -> "SessionBuilder":
+        """Frame of each remote handle's first input (the peers' input delay)."""
+        self._remote_delay = int(delay)
+        return self
+
+    def start_p2p_session(self) -> "P2PSession":  # :251-308
+        from .p2p import P2PSession, PlayerType
+        players = getattr(self, "_players", {})
+        n = int(self._cfg.num_players)
+        for h in range(n):
+            if h not in players:
+                raise InvalidRequest("Not enough players have been added. Keep registering players up to the "
+                                     "defined player number.")
+        if any(h >= n for h in players):
+            raise InvalidRequest("The player handle you provided is invalid. For a local player, the handle "
+                                 "should be between 0 and num_players")
+        pc = L.RbP2PConfig()
+        lib = L.load()
+        lib.rb_p2p_config_init(ctypes.byref(pc))
+        pc.game = self._cfg.game
+        pc.num_sessions = self._cfg.num_sessions
+        pc.num_players = n
+        pc.max_prediction = self._cfg.max_prediction
+        pc.input_delay = self._cfg.input_delay
+        pc.device = self._cfg.device
+        pc.local_mask = sum(1 << h for h, t in players.items() if t == PlayerType.Local)
+        pc.remote_delay = getattr(self, "_remote_delay", 0)
+        pc.sparse_saving = int(getattr(self, "_sparse", False))
+        pc.flags = self._cfg.flags & L.RB_FLAG_LANE_PER_SESSION
+        pc.block_size = self._cfg.block_size
+        h = ctypes.c_void_p()
+        st = lib.rb_p2p_create(ctypes.byref(pc), ctypes.byref(h))
+        if st != L.RB_OK:
+            msg = (lib.rb_p2p_last_error(None) or b"").decode()
+            raise InvalidRequest(msg) if st == L.RB_INVALID_REQUEST else DeviceError(msg)
+        return P2PSession(lib, h, Game(pc.game), pc)
+
     def start_synctest_session(self) -> "SyncTestSession":  # :342-354
         lib = L.load()
         h = ctypes.c_void_p()

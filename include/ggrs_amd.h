@@ -196,6 +196,81 @@ rb_status rb_debug_speed_clamp(int32_t device, const float* vx, const float* vy,
 rb_status rb_profile_enable(rb_batch* b, int32_t on);
 rb_status rb_profile_take(rb_batch* b, double* total_ms, int32_t* launches);
 
+/* ===========================================================================
+ * P2PSession batches (sessions/p2p_session.rs) — the rollback path.
+ *
+ * S independent P2P sessions seen from one peer, each with num_players
+ * handles: bit h of local_mask set = add_player(PlayerType::Local, h), clear =
+ * PlayerType::Remote (builder.rs:90-128).  The network layer is not part of
+ * the batch: UdpProtocol's role on this path, turning packets into
+ * Event::Input{input, player} in frame order (p2p_session.rs:838-852), is the
+ * caller's: per tick and remote handle it passes the newest delivered frame
+ * (`remote_upto`) and the inputs by frame (`remote_inputs`).  Mispredicted
+ * remote inputs roll sessions back individually (per-session depth), on the
+ * device.  Spectators, time sync and disconnects are out of scope.
+ * ======================================================================== */
+typedef struct rb_p2p rb_p2p;
+
+typedef struct rb_p2p_config {
+  int32_t abi_version;    /* = RB_ABI_VERSION */
+  int32_t game;           /* rb_game: RB_GAME_EX_GAME, RB_GAME_STUB, RB_GAME_BRAWLER */
+  int32_t num_sessions;
+  int32_t num_players;    /* with_num_players (builder.rs:154-157) */
+  int32_t max_prediction; /* with_max_prediction_window (builder.rs:136-145) */
+  int32_t input_delay;    /* with_input_delay (builder.rs:148-151): local handles */
+  int32_t device;
+  uint32_t local_mask;    /* bit h: handle h is PlayerType::Local; at least one local and one remote */
+  int32_t remote_delay;   /* frame of each remote handle's first Event::Input (the peer's input delay) */
+  int32_t sparse_saving;  /* with_sparse_saving_mode (builder.rs:159-166) */
+  uint32_t flags;         /* RB_FLAG_LANE_PER_SESSION only */
+  uint32_t block_size;
+  uint32_t reserved[4];
+} rb_p2p_config;
+
+/* SessionBuilder::new() defaults for a 2-player session, handle 0 local, handle 1 remote. */
+void rb_p2p_config_init(rb_p2p_config* cfg);
+
+/* SessionBuilder::start_p2p_session (builder.rs:251-308) for S sessions that
+ * start Running (the synchronisation handshake is the network's). */
+rb_status rb_p2p_create(const rb_p2p_config* cfg, rb_p2p** out);
+void rb_p2p_destroy(rb_p2p* b);
+const char* rb_p2p_last_error(const rb_p2p* b);
+rb_status rb_p2p_set_stream(rb_p2p* b, void* hip_stream);
+
+/* n_ticks x [poll_remote_clients + add_local_input for every local handle +
+ * advance_frame (p2p_session.rs:253-337) + handle_requests] for every session,
+ * in ONE device launch.  Device pointers, stream ordered:
+ *   local_inputs  tick t, handle h: local_inputs + t*local_stride_bytes + (h*S + s)*input_bytes
+ *                 (entries of remote handles are ignored)
+ *   remote_upto   int32 [n_ticks][num_players][S]: newest frame delivered for
+ *                 remote handle h before tick t's advance_frame (monotone;
+ *                 entries of local handles ignored)
+ *   remote_inputs [remote_frames][num_players][S] Input values by frame
+ * A session that hits PredictionThreshold (sync_layer.rs:163-167) does not
+ * advance that tick (rb_p2p_read_status reports it), exactly as the
+ * reference's advance_frame returns Err: its bookkeeping moves, its game does
+ * not.  Asynchronous (stream ordered): a session that hits a reference assert
+ * stops and reports RB_PANIC through rb_p2p_read_status / rb_p2p_counters. */
+rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs, int64_t local_stride_bytes,
+                           const int32_t* remote_upto, const void* remote_inputs, int32_t remote_frames);
+
+/* Per session, the last tick: rb_status of its advance_frame, the LoadGameState
+ * frame (RB_NULL_FRAME: no rollback), AdvanceFrame and SaveGameState counts.
+ * Any pointer may be NULL.  Synchronises. */
+rb_status rb_p2p_read_status(rb_p2p* b, int32_t* status, int32_t* load_frame, int32_t* n_advance, int32_t* n_save);
+/* SyncLayer::current_frame and last_confirmed_frame per session.  Synchronises. */
+rb_status rb_p2p_read_frames(rb_p2p* b, int32_t* current, int32_t* confirmed);
+/* All cells: frame tags [W][S], images [W][S][rb_p2p_state_bytes], checksums [W][S][2]. */
+rb_status rb_p2p_read_cells(rb_p2p* b, int32_t* tags, void* images, uint64_t* checksums);
+/* The game state after the last advance, images [S][rb_p2p_state_bytes] (frame word = current frame). */
+rb_status rb_p2p_read_live(rb_p2p* b, void* images);
+int32_t rb_p2p_state_bytes(const rb_p2p* b);
+/* Counters since create: [0] PredictionThreshold hits, [1] unexpected math paths, [2] panicked sessions. */
+rb_status rb_p2p_counters(rb_p2p* b, uint32_t* out3);
+/* HIP event timing of every rb_p2p_run_ticks launch (bench.py): total ms and launches since the last take. */
+rb_status rb_p2p_profile_enable(rb_p2p* b, int32_t on);
+rb_status rb_p2p_profile_take(rb_p2p* b, double* total_ms, int32_t* launches);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

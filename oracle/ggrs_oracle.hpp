@@ -475,6 +475,132 @@ class SyncTestSession {
   }
 };
 
+// ---------------------------------------------------------------------------
+// sessions/p2p_session.rs  P2PSession<T> — the rollback path without the
+// network layer.  UdpProtocol's job on this path is to turn packets into
+// Event::Input{input, player} in frame order (handle_event, :838-852); here the
+// caller delivers those inputs directly (deliver_remote_input).  Spectators,
+// time sync / wait recommendations, desync-report messages and the
+// synchronisation handshake (the session starts Running) are out of scope
+// (DESIGN.md §7); disconnects are not modelled (disconnect_frame stays NULL).
+// ---------------------------------------------------------------------------
+template <class C>
+class P2PSession {
+ public:
+  using I = typename C::Input;
+  size_t num_players, max_prediction;
+  bool sparse_saving;
+  SyncLayer<C> sync_layer;
+  std::vector<ConnectionStatus> local_connect_status;
+  std::vector<bool> is_local;
+  Frame disconnect_frame = NULL_FRAME;
+  std::map<PlayerHandle, PlayerInput<I>> local_inputs;
+
+  // :160-213 (local players get the input delay; remote queues have none)
+  P2PSession(size_t np, size_t mp, bool sparse, size_t delay, std::vector<bool> local)
+      : num_players(np), max_prediction(mp), sparse_saving(sparse), sync_layer(np, mp),
+        local_connect_status(np), is_local(std::move(local)) {
+    for (size_t h = 0; h < np; ++h)
+      if (is_local[h]) sync_layer.set_frame_delay(h, delay);
+  }
+
+  Error add_local_input(PlayerHandle h, I input) {  // :223-240
+    if (h >= num_players || !is_local[h])
+      return Error::invalid("The player handle you provided is not referring to a local player.");
+    local_inputs[h] = PlayerInput<I>(sync_layer.current_frame(), input);
+    return Error::ok();
+  }
+
+  // handle_event(Event::Input{input, player}) (:838-852)
+  void deliver_remote_input(PlayerHandle player, PlayerInput<I> input) {
+    ORC_ASSERT(player < num_players);
+    if (!local_connect_status[player].disconnected) {
+      Frame cur = local_connect_status[player].last_frame;
+      ORC_ASSERT(cur == NULL_FRAME || cur + 1 == input.frame);
+      local_connect_status[player].last_frame = input.frame;
+      sync_layer.add_remote_input(player, input);
+    }
+  }
+
+  Frame confirmed_frame() const {  // :487-498
+    Frame cf = INT32_MAX;
+    for (auto& c : local_connect_status)
+      if (!c.disconnected) cf = std::min(cf, c.last_frame);
+    ORC_ASSERT(cf < INT32_MAX);
+    return cf;
+  }
+  Frame current_frame() const { return sync_layer.current_frame(); }
+
+  // :253-337 (poll_remote_clients = the deliveries made before this call)
+  Error advance_frame(std::vector<Request<C>>& requests) {
+    requests.clear();
+    if (sync_layer.current_frame() == 0) requests.push_back(sync_layer.save_current_state());
+    Frame confirmed = confirmed_frame();
+    Frame first_incorrect = sync_layer.check_simulation_consistency(disconnect_frame);
+    if (first_incorrect != NULL_FRAME) {
+      adjust_gamestate(first_incorrect, confirmed, requests);
+      disconnect_frame = NULL_FRAME;
+    }
+    Frame last_saved = sync_layer.last_saved_frame;
+    if (sparse_saving)
+      check_last_saved_state(last_saved, confirmed, requests);
+    else
+      requests.push_back(sync_layer.save_current_state());
+    sync_layer.set_last_confirmed_frame(confirmed, sparse_saving);
+    for (size_t h = 0; h < num_players; ++h) {  // local_player_handles()
+      if (!is_local[h]) continue;
+      auto it = local_inputs.find(h);
+      if (it == local_inputs.end()) return Error::invalid("Missing local input while calling advance_frame().");
+      Frame actual = NULL_FRAME;
+      Error e = sync_layer.add_local_input(h, it->second, &actual);
+      if (e.is_err()) return e;
+      ORC_ASSERT(actual != NULL_FRAME);
+      it->second.frame = actual;
+      local_connect_status[h].last_frame = actual;
+    }
+    local_inputs.clear();
+    auto inputs = sync_layer.synchronized_inputs(local_connect_status);
+    Frame from = sync_layer.current_frame();
+    sync_layer.advance_frame();
+    requests.push_back(Request<C>{RequestKind::Advance, {}, from, std::move(inputs)});
+    return Error::ok();
+  }
+
+ private:
+  void adjust_gamestate(Frame first_incorrect, Frame min_confirmed, std::vector<Request<C>>& requests) {  // :621-673
+    Frame current = sync_layer.current_frame();
+    Frame frame_to_load = sparse_saving ? sync_layer.last_saved_frame : first_incorrect;
+    ORC_ASSERT(frame_to_load <= first_incorrect);
+    Frame count = current - frame_to_load;
+    requests.push_back(sync_layer.load_frame(frame_to_load));
+    ORC_ASSERT(sync_layer.current_frame() == frame_to_load);
+    sync_layer.reset_prediction();
+    for (Frame i = 0; i < count; ++i) {
+      auto inputs = sync_layer.synchronized_inputs(local_connect_status);
+      if (sparse_saving) {
+        if (sync_layer.current_frame() == min_confirmed) requests.push_back(sync_layer.save_current_state());
+      } else if (i > 0) {
+        requests.push_back(sync_layer.save_current_state());
+      }
+      Frame from = sync_layer.current_frame();
+      sync_layer.advance_frame();
+      requests.push_back(Request<C>{RequestKind::Advance, {}, from, std::move(inputs)});
+    }
+    ORC_ASSERT(sync_layer.current_frame() == current);
+  }
+
+  void check_last_saved_state(Frame last_saved, Frame confirmed, std::vector<Request<C>>& requests) {  // :778-802
+    if (sync_layer.current_frame() - last_saved >= static_cast<Frame>(max_prediction)) {
+      if (confirmed >= sync_layer.current_frame())
+        requests.push_back(sync_layer.save_current_state());
+      else
+        adjust_gamestate(last_saved, confirmed, requests);
+      ORC_ASSERT(confirmed == NULL_FRAME ||
+                 sync_layer.last_saved_frame == std::min(confirmed, sync_layer.current_frame()));
+    }
+  }
+};
+
 // builder.rs:13-27, 136-157, 202-205, 342-354 — the SyncTest subset
 struct SessionBuilder {
   size_t num_players = 2;        // DEFAULT_PLAYERS

@@ -51,6 +51,16 @@ def load():
             "orc_synth_inputs": (None, [U64, ctypes.c_uint32, I32, I32, I32, I32, I32, P]),
             "orc_bench_exgame": (ctypes.c_double, [I32, I32, I32, I32, I32, I32, I32, I32, U64, PI32]),
             "orc_bench_brawler": (ctypes.c_double, [I32, I32, I32, I32, I32, I32, I32, I32, U64, PI32]),
+            "orc_p2p_create": (P, [I32, I32, I32, I32, ctypes.c_uint32, I32, I32, I32]),
+            "orc_p2p_destroy": (None, [P]),
+            "orc_p2p_last_panic": (ctypes.c_char_p, [P]),
+            "orc_p2p_deliver": (I32, [P, I32, P, P, I32]),
+            "orc_p2p_add_local_input": (I32, [P, I32, P]),
+            "orc_p2p_advance": (I32, [P, P, P, P, P]),
+            "orc_p2p_trace": (I32, [P, I32, PI32, PI32, I32]),
+            "orc_p2p_read_cells": (I32, [P, P, P, P]),
+            "orc_p2p_read_live": (I32, [P, P, P]),
+            "orc_p2p_frames": (I32, [P, P, P]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
@@ -132,6 +142,82 @@ class OracleBatch:
     def corrupt_cell(self, session: int, frame: int, word: int, xor_mask: int) -> None:
         rc = self._lib.orc_batch_corrupt_cell(self._h, session, frame, word, xor_mask & 0xFFFFFFFF)
         assert rc == 0, "no cell holds that frame"
+
+
+class OracleP2P:
+    """S independent network-free reference P2PSessions + games (TEST ONLY).
+
+    Per tick: deliver(handle, upto, by_frame) for every remote handle (the
+    Event::Input stream poll_remote_clients would produce: frames up to
+    upto[s], values by_frame[f, s]), add_local_input for every local handle,
+    advance()."""
+
+    def __init__(self, game: int, num_players: int, max_prediction: int, input_delay: int, local_mask: int,
+                 num_sessions: int, sparse_saving: bool = False, remote_delay: int = 0):
+        lib = load()
+        self._lib = lib
+        self._h = lib.orc_p2p_create(game, num_players, max_prediction, input_delay, local_mask,
+                                     int(sparse_saving), remote_delay, num_sessions)
+        if not self._h:
+            raise ValueError(lib.orc_last_error().decode())
+        self.game, self.P, self.W, self.S = game, num_players, max_prediction, num_sessions
+        self.image_bytes = lib.orc_image_bytes(game, num_players)
+        self.input_dtype = np.uint32 if lib.orc_input_bytes(game) == 4 else np.uint8
+
+    def close(self):
+        if self._h:
+            self._lib.orc_p2p_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def last_panic(self) -> str:
+        return self._lib.orc_p2p_last_panic(self._h).decode()
+
+    def deliver(self, handle: int, upto, by_frame) -> int:
+        u = np.ascontiguousarray(np.broadcast_to(np.asarray(upto), (self.S,)), dtype=np.int32)
+        b = np.ascontiguousarray(by_frame, dtype=self.input_dtype)
+        assert b.ndim == 2 and b.shape[1] == self.S
+        return self._lib.orc_p2p_deliver(self._h, handle, _ptr(u), _ptr(b), b.shape[0])
+
+    def add_local_input(self, handle: int, inputs) -> int:
+        a = np.ascontiguousarray(np.broadcast_to(np.asarray(inputs), (self.S,)), dtype=self.input_dtype)
+        return self._lib.orc_p2p_add_local_input(self._h, handle, _ptr(a))
+
+    def advance(self):
+        """(status [S] (0 Ok, 1 PredictionThreshold, 99 panic), load frame [S], AdvanceFrames [S], saves [S])."""
+        st, lf, na, ns = (np.empty(self.S, np.int32) for _ in range(4))
+        self._lib.orc_p2p_advance(self._h, _ptr(st), _ptr(lf), _ptr(na), _ptr(ns))
+        return st, lf, na, ns
+
+    def trace(self, session: int = 0):
+        cap = 6 * self.W + 8
+        k = (ctypes.c_int32 * cap)()
+        f = (ctypes.c_int32 * cap)()
+        n = self._lib.orc_p2p_trace(self._h, session, k, f, cap)
+        return [(k[i], f[i]) for i in range(n)]
+
+    def read_cells(self):
+        """(cell frames [W, S], images [W, S, B], checksums [W, S, 2])."""
+        fr = np.empty((self.W, self.S), np.int32)
+        img = np.zeros((self.W, self.S, self.image_bytes), np.uint8)
+        cs = np.zeros((self.W, self.S, 2), np.uint64)
+        self._lib.orc_p2p_read_cells(self._h, _ptr(fr), _ptr(img), _ptr(cs))
+        return fr, img, cs
+
+    def read_live(self):
+        """(images [S, B], current frames [S])."""
+        img = np.zeros((self.S, self.image_bytes), np.uint8)
+        fr = np.zeros(self.S, np.int32)
+        self._lib.orc_p2p_read_live(self._h, _ptr(img), _ptr(fr))
+        return img, fr
+
+    def frames(self):
+        """(current frames [S], last confirmed frames [S])."""
+        c = np.empty(self.S, np.int32)
+        k = np.empty(self.S, np.int32)
+        self._lib.orc_p2p_frames(self._h, _ptr(c), _ptr(k))
+        return c, k
 
 
 def fletcher16(data: bytes) -> int:

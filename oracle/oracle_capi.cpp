@@ -191,6 +191,161 @@ struct Batch : BatchBase {
   }
 };
 
+// S independent network-free P2PSessions (ggrs_oracle.hpp P2PSession) + their
+// games, driven like ex_game_p2p.rs:105-125: deliver the remote inputs that
+// "arrived" (poll_remote_clients), add_local_input for every local handle,
+// advance_frame, handle_requests.
+struct P2PBatchBase {
+  virtual ~P2PBatchBase() = default;
+  virtual int32_t deliver(int32_t handle, const int32_t* upto, const uint8_t* by_frame, int32_t n_frames) = 0;
+  virtual int32_t add_local_input(int32_t handle, const uint8_t* inputs) = 0;
+  virtual int32_t advance(int32_t* status, int32_t* load_frame, int32_t* n_adv, int32_t* n_save) = 0;
+  virtual int32_t trace(int32_t session, int32_t* kinds, int32_t* frames, int32_t cap) = 0;
+  virtual int32_t read_cells(int32_t* cell_frames, uint8_t* images, uint64_t* cs) = 0;
+  virtual int32_t read_live(uint8_t* images, int32_t* frames) = 0;
+  virtual int32_t frames(int32_t* current, int32_t* confirmed) = 0;
+  std::string last_panic;
+};
+
+template <class C, class G>
+struct P2PBatch : P2PBatchBase {
+  using I = typename C::Input;
+  std::vector<std::unique_ptr<P2PSession<C>>> sess;
+  std::vector<G> games;
+  std::vector<std::vector<Request<C>>> last_reqs;
+  int32_t remote_first;  // frame of a remote's first input (the remote's input delay)
+  size_t max_pred;
+
+  template <class MakeGame>
+  P2PBatch(int32_t P, int32_t W, int32_t delay, uint32_t local_mask, bool sparse, int32_t remote_delay, int32_t S,
+           MakeGame mk)
+      : remote_first(remote_delay), max_pred(static_cast<size_t>(W)) {
+    std::vector<bool> local(static_cast<size_t>(P));
+    for (int32_t h = 0; h < P; ++h) local[h] = (local_mask >> h) & 1u;
+    for (int32_t s = 0; s < S; ++s) {
+      sess.push_back(std::make_unique<P2PSession<C>>(P, W, sparse, delay, local));
+      games.push_back(mk(s));
+    }
+    last_reqs.resize(S);
+  }
+
+  int32_t deliver(int32_t handle, const int32_t* upto, const uint8_t* by_frame, int32_t n_frames) override {
+    const size_t S = sess.size();
+    try {
+      for (size_t s = 0; s < S; ++s) {
+        auto& ss = *sess[s];
+        Frame last = ss.local_connect_status.at(handle).last_frame;
+        Frame f0 = last == NULL_FRAME ? remote_first : last + 1;
+        for (Frame f = f0; f <= upto[s]; ++f) {
+          if (f >= n_frames) throw Panic("deliver: frame beyond the provided inputs");
+          I v{};
+          std::memcpy(&v, by_frame + (static_cast<size_t>(f) * S + s) * sizeof(I), sizeof(I));
+          ss.deliver_remote_input(static_cast<PlayerHandle>(handle), PlayerInput<I>(f, v));
+        }
+      }
+    } catch (const Panic& p) {
+      last_panic = p.what();
+      return KIND_PANIC;
+    }
+    return 0;
+  }
+
+  int32_t add_local_input(int32_t handle, const uint8_t* in) override {
+    int32_t first = 0;
+    for (size_t s = 0; s < sess.size(); ++s) {
+      I v{};
+      std::memcpy(&v, in + s * sizeof(I), sizeof(I));
+      Error e = sess[s]->add_local_input(static_cast<PlayerHandle>(handle), v);
+      if (e.is_err() && first == 0) first = static_cast<int32_t>(e.kind);
+    }
+    return first;
+  }
+
+  int32_t advance(int32_t* status, int32_t* load_frame, int32_t* n_adv, int32_t* n_save) override {
+    int32_t nerr = 0;
+    for (size_t s = 0; s < sess.size(); ++s) {
+      int32_t k = 0;
+      try {
+        Error e = sess[s]->advance_frame(last_reqs[s]);
+        if (e.is_err()) k = static_cast<int32_t>(e.kind);
+        // on Err the requests built before the failure stay in the Vec the
+        // reference drops; the game never sees them, but the session's
+        // bookkeeping (rollback, saves) has happened (p2p_session.rs:253-337)
+        if (!e.is_err()) games[s].handle_requests(last_reqs[s]);
+        else last_reqs[s].clear();
+      } catch (const Panic& p) {
+        k = KIND_PANIC;
+        last_panic = p.what();
+      }
+      Frame lf = NULL_FRAME;
+      int32_t na = 0, ns = 0;
+      for (auto& r : last_reqs[s]) {
+        if (r.kind == RequestKind::Load) lf = r.frame;
+        na += r.kind == RequestKind::Advance;
+        ns += r.kind == RequestKind::Save;
+      }
+      if (k) ++nerr;
+      if (status) status[s] = k;
+      if (load_frame) load_frame[s] = lf;
+      if (n_adv) n_adv[s] = na;
+      if (n_save) n_save[s] = ns;
+    }
+    return nerr;
+  }
+
+  int32_t trace(int32_t session, int32_t* kinds, int32_t* frames, int32_t cap) override {
+    auto& r = last_reqs.at(session);
+    int32_t n = static_cast<int32_t>(r.size());
+    for (int32_t i = 0; i < n && i < cap; ++i) {
+      kinds[i] = static_cast<int32_t>(r[i].kind);
+      frames[i] = r[i].frame;
+    }
+    return n;
+  }
+
+  // cells [W][S]: per-session frame tag, image, checksum (lo, hi)
+  int32_t read_cells(int32_t* cell_frames, uint8_t* images, uint64_t* cs) override {
+    const size_t S = sess.size();
+    size_t img = 0;
+    for (size_t w = 0; w < max_pred; ++w)
+      for (size_t s = 0; s < S; ++s) {
+        const auto& cell = sess[s]->sync_layer.saved_states.states[w];
+        if (cell_frames) cell_frames[w * S + s] = cell.frame();
+        auto d = cell.load();
+        if (d) {
+          auto v = image_of(*d);
+          img = v.size();
+          if (images) std::memcpy(images + (w * S + s) * img, v.data(), img);
+        }
+        u128 x = cell.checksum().value_or(0);
+        if (cs) {
+          cs[(w * S + s) * 2 + 0] = static_cast<uint64_t>(x);
+          cs[(w * S + s) * 2 + 1] = static_cast<uint64_t>(x >> 64);
+        }
+      }
+    return static_cast<int32_t>(img);
+  }
+
+  int32_t read_live(uint8_t* images, int32_t* frames_out) override {
+    size_t img = 0;
+    for (size_t s = 0; s < sess.size(); ++s) {
+      auto v = image_of(live_of(games[s]));
+      img = v.size();
+      if (images) std::memcpy(images + s * img, v.data(), img);
+      if (frames_out) frames_out[s] = sess[s]->current_frame();
+    }
+    return static_cast<int32_t>(img);
+  }
+
+  int32_t frames(int32_t* current, int32_t* confirmed) override {
+    for (size_t s = 0; s < sess.size(); ++s) {
+      if (current) current[s] = sess[s]->current_frame();
+      if (confirmed) confirmed[s] = sess[s]->sync_layer.last_confirmed_frame;
+    }
+    return 0;
+  }
+};
+
 thread_local std::string g_err;
 
 }  // namespace
@@ -249,6 +404,56 @@ int32_t orc_batch_read_live(void* b, uint8_t* images, uint64_t* last_cs, int32_t
   return static_cast<BatchBase*>(b)->read_live(images, last_cs, last_cs_frame);
 }
 int32_t orc_batch_current_frame(void* b) { return static_cast<BatchBase*>(b)->current_frame(); }
+
+// Network-free P2P batches (P2PBatch above).  local_mask: bit h set = handle h
+// is local; remote_delay: frame of every remote's first input.
+void* orc_p2p_create(int32_t game, int32_t num_players, int32_t max_prediction, int32_t input_delay,
+                     uint32_t local_mask, int32_t sparse, int32_t remote_delay, int32_t num_sessions) {
+  try {
+    if (max_prediction <= 0) { g_err = "Currently, only prediction windows above 0 are supported"; return nullptr; }
+    const bool sp = sparse != 0;
+    switch (game) {
+      case EX_GAME:
+        return new P2PBatch<exgame::Config, exgame::Game>(num_players, max_prediction, input_delay, local_mask, sp,
+                                                           remote_delay, num_sessions,
+                                                           [&](int32_t) { return exgame::Game(num_players); });
+      case STUB:
+        return new P2PBatch<stub::Config, stub::GameStub>(num_players, max_prediction, input_delay, local_mask, sp,
+                                                          remote_delay, num_sessions, [&](int32_t) { return stub::GameStub{}; });
+      case BRAWLER:
+        return new P2PBatch<brawler::Config, brawler::Game>(num_players, max_prediction, input_delay, local_mask, sp,
+                                                            remote_delay, num_sessions,
+                                                            [&](int32_t) { return brawler::Game(num_players); });
+      default: g_err = "unknown game for p2p"; return nullptr;
+    }
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return nullptr;
+  }
+}
+void orc_p2p_destroy(void* b) { delete static_cast<P2PBatchBase*>(b); }
+const char* orc_p2p_last_panic(void* b) { return static_cast<P2PBatchBase*>(b)->last_panic.c_str(); }
+int32_t orc_p2p_deliver(void* b, int32_t handle, const int32_t* upto, const uint8_t* by_frame, int32_t n_frames) {
+  return static_cast<P2PBatchBase*>(b)->deliver(handle, upto, by_frame, n_frames);
+}
+int32_t orc_p2p_add_local_input(void* b, int32_t handle, const uint8_t* inputs) {
+  return static_cast<P2PBatchBase*>(b)->add_local_input(handle, inputs);
+}
+int32_t orc_p2p_advance(void* b, int32_t* status, int32_t* load_frame, int32_t* n_adv, int32_t* n_save) {
+  return static_cast<P2PBatchBase*>(b)->advance(status, load_frame, n_adv, n_save);
+}
+int32_t orc_p2p_trace(void* b, int32_t session, int32_t* kinds, int32_t* frames, int32_t cap) {
+  return static_cast<P2PBatchBase*>(b)->trace(session, kinds, frames, cap);
+}
+int32_t orc_p2p_read_cells(void* b, int32_t* cell_frames, uint8_t* images, uint64_t* cs) {
+  return static_cast<P2PBatchBase*>(b)->read_cells(cell_frames, images, cs);
+}
+int32_t orc_p2p_read_live(void* b, uint8_t* images, int32_t* frames) {
+  return static_cast<P2PBatchBase*>(b)->read_live(images, frames);
+}
+int32_t orc_p2p_frames(void* b, int32_t* current, int32_t* confirmed) {
+  return static_cast<P2PBatchBase*>(b)->frames(current, confirmed);
+}
 
 // Third-party arithmetic, exposed for the known-answer tests.
 uint16_t orc_fletcher16(const uint8_t* d, uint64_t n) { return fletcher16(d, n); }

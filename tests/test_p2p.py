@@ -1,0 +1,206 @@
+"""P2PSession rollback: the network-free oracle restatement
+(oracle/ggrs_oracle.hpp P2PSession) and, on the GPU, the device batch
+(ggrs_amd/csrc/p2p.hpp) against it.
+
+Pinning: the reference's own P2P test (tests/test_p2p_session.rs:97-145, two
+peers exchanging inputs: game frame == i + 1 after every advance) is restated
+with two oracle sessions delivering to each other.  Beyond that the oracle is
+a restatement (parity unpinned numerically, as for SyncTest), checked here by
+a property every correct rollback must have: the cells of confirmed frames
+equal those of a run in which every remote input arrived before it was needed.
+"""
+import numpy as np
+import pytest
+
+import ggrs_amd as G
+from ggrs_amd.p2p import PlayerType, synth_network
+from oracle import oracle as O
+
+ORC_GAME = {G.Game.EX_GAME: O.EX_GAME, G.Game.STUB: O.STUB, G.Game.BRAWLER: O.BRAWLER}
+
+
+def drive_oracle(orc, local_mask, inputs, upto, remote_in, T, t0=0):
+    """Ticks [t0, T) of the oracle batch; returns per-tick (status, load, nadv, nsave)."""
+    out = []
+    P = inputs.shape[1]
+    for t in range(t0, T):
+        for h in range(P):
+            if not (local_mask >> h) & 1:
+                assert orc.deliver(h, upto[t, h], remote_in[:, h, :]) == 0, orc.last_panic()
+        for h in range(P):
+            if (local_mask >> h) & 1:
+                assert orc.add_local_input(h, inputs[t, h]) == 0
+        out.append(orc.advance())
+    return out
+
+
+# ---------------------------------------------------------------------------- oracle (CPU)
+def test_oracle_two_peers_advance_like_reference_test():
+    # tests/test_p2p_session.rs:97-145: sess1 (local 0, remote 1) and sess2
+    # (remote 0, local 1) exchange StubInput{inp: i}; after each advance both
+    # games are at frame i + 1.  Inputs sent by one peer reach the other before
+    # its next advance (the poll_remote_clients of the next iteration).
+    s1 = O.OracleP2P(O.STUB, 2, 8, 0, 0b01, 1)
+    s2 = O.OracleP2P(O.STUB, 2, 8, 0, 0b10, 1)
+    sent1, sent2 = [], []  # inputs each peer added, by frame
+    for i in range(10):
+        if sent2:
+            s1.deliver(1, [len(sent2) - 1], np.array(sent2, np.uint32)[:, None])
+        if sent1:
+            s2.deliver(0, [len(sent1) - 1], np.array(sent1, np.uint32)[:, None])
+        s1.add_local_input(0, [i])
+        st, _, _, _ = s1.advance()
+        assert st[0] == 0
+        sent1.append(i)
+        s2.add_local_input(1, [i])
+        st, _, _, _ = s2.advance()
+        assert st[0] == 0
+        sent2.append(i)
+        img1, fr1 = s1.read_live()
+        img2, fr2 = s2.read_live()
+        assert int(np.frombuffer(img1[0, :4].tobytes(), np.int32)[0]) == i + 1
+        assert int(np.frombuffer(img2[0, :4].tobytes(), np.int32)[0]) == i + 1
+
+
+@pytest.mark.parametrize("game", [G.Game.STUB, G.Game.EX_GAME])
+@pytest.mark.parametrize("sparse", [False, True])
+def test_oracle_rollback_reaches_the_confirmed_truth(game, sparse):
+    S, P, W, T, mask = 16, 2, 8, 120, 0b01
+    dt = np.uint32 if game == G.Game.STUB else np.uint8
+    inputs, upto, rin = synth_network(S, P, T, mask, remote_delay=1, min_lag=1, max_lag=5, dtype=dt,
+                                      mask=0x3 if game == G.Game.STUB else 0x0F)
+    lag = O.OracleP2P(ORC_GAME[game], P, W, 2, mask, S, sparse_saving=sparse, remote_delay=1)
+    res = drive_oracle(lag, mask, inputs, upto, rin, T)
+    assert all((r[0] == 0).all() for r in res), "no PredictionThreshold / panic expected"
+    loads = np.array([r[1] for r in res])
+    assert (loads != G.NULL_FRAME).sum() > S, "the schedule must cause rollbacks"
+    # ground truth: every remote input delivered before the first advance
+    truth = O.OracleP2P(ORC_GAME[game], P, W, 2, mask, S, sparse_saving=False, remote_delay=1)
+    full = np.full((T, P, S), T, np.int32)
+    seen = {}  # (session, frame) -> (image, checksum) of every cell the truth run saved
+    for t in range(T):
+        r = drive_oracle(truth, mask, inputs, full, rin, t + 1, t0=t)[0]
+        assert (r[1] == G.NULL_FRAME).all(), "no rollback with everything delivered"
+        ttags, timgs, tcs = truth.read_cells()
+        for w in range(W):
+            for s in range(S):
+                if ttags[w, s] >= 0:
+                    seen[(s, int(ttags[w, s]))] = (timgs[w, s].copy(), tcs[w, s].copy())
+    cur, conf = lag.frames()
+    tags, imgs, cs = lag.read_cells()
+    checked = 0
+    for s in range(S):
+        for w in range(W):
+            f = int(tags[w, s])
+            if f < 0 or f > conf[s]:
+                continue
+            timg, tc = seen[(s, f)]
+            np.testing.assert_array_equal(imgs[w, s], timg, err_msg=f"session {s} frame {f}")
+            assert (cs[w, s] == tc).all()
+            checked += 1
+    assert checked >= S
+
+
+def test_oracle_prediction_threshold_drops_the_requests():
+    # A peer that stops sending: after max_prediction frames advance_frame
+    # returns PredictionThreshold and the game no longer moves.
+    S, P, W, T, mask = 4, 2, 4, 12, 0b01
+    inputs, upto, rin = synth_network(S, P, T, mask, remote_delay=0, min_lag=1, max_lag=1)
+    upto[:] = np.where(np.arange(T)[:, None, None] < 3, upto, upto[2])  # deliveries stop after tick 2
+    orc = O.OracleP2P(O.EX_GAME, P, W, 0, mask, S)
+    res = drive_oracle(orc, mask, inputs, upto, rin, T)
+    st = np.array([r[0] for r in res])
+    assert (st[-1] == 1).all() and (st[0] == 0).all()
+    cur, _ = orc.frames()
+    assert (cur < T).all()
+
+
+# ---------------------------------------------------------------------------- device vs oracle
+def gpu_pair(game, S, P, W, d, rd, mask, sparse, lane_per_session=False):
+    b = (G.SessionBuilder(game, num_sessions=S).with_num_players(P).with_max_prediction_window(W)
+         .with_input_delay(d).with_sparse_saving_mode(sparse).with_remote_input_delay(rd)
+         .with_lane_per_session(lane_per_session))
+    for h in range(P):
+        b.add_player(PlayerType.Local if (mask >> h) & 1 else PlayerType.Remote, h)
+    sess = b.start_p2p_session()
+    orc = O.OracleP2P(ORC_GAME[game], P, W, d, mask, S, sparse_saving=sparse, remote_delay=rd)
+    return sess, orc
+
+
+def compare_state(sess, orc, tick):
+    tags, imgs, cs = sess.read_cells()
+    otags, oimgs, ocs = orc.read_cells()
+    np.testing.assert_array_equal(tags, otags, err_msg=f"cell frames, tick {tick}")
+    valid = otags >= 0
+    np.testing.assert_array_equal(imgs[valid], oimgs[valid], err_msg=f"cell images, tick {tick}")
+    np.testing.assert_array_equal(cs[valid], ocs[valid], err_msg=f"cell checksums, tick {tick}")
+    np.testing.assert_array_equal(sess.read_live(), orc.read_live()[0], err_msg=f"live state, tick {tick}")
+    c, k = sess.frames()
+    oc, ok = orc.frames()
+    np.testing.assert_array_equal(c, oc)
+    np.testing.assert_array_equal(k, ok)
+
+
+CASES = [  # game, P, W, d, rd, local_mask, sparse, lag range
+    (G.Game.EX_GAME, 2, 8, 0, 0, 0b01, False, (1, 4)),
+    (G.Game.EX_GAME, 2, 8, 2, 2, 0b01, False, (0, 6)),
+    (G.Game.EX_GAME, 2, 8, 2, 1, 0b10, True, (1, 5)),
+    (G.Game.EX_GAME, 4, 8, 1, 1, 0b0001, False, (1, 5)),
+    (G.Game.EX_GAME, 3, 7, 0, 2, 0b010, True, (0, 4)),
+    (G.Game.STUB, 2, 8, 1, 0, 0b01, False, (1, 5)),
+    (G.Game.STUB, 2, 6, 0, 1, 0b10, True, (1, 4)),
+    (G.Game.EX_GAME, 2, 4, 0, 0, 0b01, False, (1, 6)),  # lags past the window: PredictionThreshold
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES, ids=[f"{c[0].name}-P{c[1]}-W{c[2]}-d{c[3]}-rd{c[4]}-m{c[5]}-sp{int(c[6])}"
+                                             for c in CASES])
+def test_gpu_p2p_matches_oracle_every_tick(gpu_available, case):
+    import torch
+    game, P, W, d, rd, mask, sparse, (lo, hi) = case
+    S, T = 70, 90
+    dt = np.uint32 if game == G.Game.STUB else np.uint8
+    inputs, upto, rin = synth_network(S, P, T, mask, rd, lo, hi, dtype=dt, mask=0x3 if game == G.Game.STUB else 0x0F)
+    sess, orc = gpu_pair(game, S, P, W, d, rd, mask, sparse)
+    di = torch.from_numpy(inputs).cuda()
+    du = torch.from_numpy(upto).cuda()
+    dr = torch.from_numpy(rin).cuda()
+    saw_rollback = saw_threshold = False
+    for t in range(T):
+        sess.run_ticks(di[t:t + 1], du[t:t + 1], dr)
+        ost, olf, ona, ons = drive_oracle(orc, mask, inputs, upto, rin, t + 1, t0=t)[0]
+        st, lf, na, ns = sess.status()
+        np.testing.assert_array_equal(st, ost, err_msg=f"status, tick {t}")
+        np.testing.assert_array_equal(lf, olf, err_msg=f"LoadGameState frame, tick {t}")
+        np.testing.assert_array_equal(na, ona, err_msg=f"AdvanceFrame count, tick {t}")
+        np.testing.assert_array_equal(ns, ons, err_msg=f"SaveGameState count, tick {t}")
+        saw_rollback |= bool((lf != G.NULL_FRAME).any())
+        saw_threshold |= bool((st == 1).any())
+        if t % 10 == 9 or t == T - 1:
+            compare_state(sess, orc, t)
+    assert saw_rollback
+    if W == 4:
+        assert saw_threshold
+    assert sess.counters()[2] == 0
+
+
+@pytest.mark.gpu
+def test_gpu_p2p_fused_launch_equals_per_tick(gpu_available):
+    # One launch of T ticks == T launches of one tick (state in registers across ticks).
+    import torch
+    game, P, W, d, rd, mask = G.Game.EX_GAME, 2, 8, 2, 1, 0b01
+    S, T = 200, 64
+    inputs, upto, rin = synth_network(S, P, T, mask, rd, 1, 5)
+    di, du, dr = (torch.from_numpy(a).cuda() for a in (inputs, upto, rin))
+    a, _ = gpu_pair(game, S, P, W, d, rd, mask, False)
+    b, orc = gpu_pair(game, S, P, W, d, rd, mask, False)
+    for t in range(T):
+        a.run_ticks(di[t:t + 1], du[t:t + 1], dr)
+    b.run_ticks(di[:T // 2], du[:T // 2], dr)
+    b.run_ticks(di[T // 2:], du[T // 2:], dr)
+    drive_oracle(orc, mask, inputs, upto, rin, T)
+    np.testing.assert_array_equal(a.read_live(), b.read_live())
+    compare_state(b, orc, T - 1)
+    for x, y in zip(a.read_cells(), b.read_cells()):
+        np.testing.assert_array_equal(x, y)
