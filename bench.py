@@ -76,6 +76,112 @@ def pmc_traffic(cfg_key):
     return best
 
 
+def bench_p2p(args):
+    """P2PSession rollback batches: every tick delivers the remote inputs that
+    arrived (synthetic lag), adds the local input and advances; sessions whose
+    predictions were wrong roll back to their first incorrect frame and
+    resimulate.  value = AdvanceFrames the games executed (resimulated + new)
+    per second, counted on the device."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import ggrs_amd as G
+    from ggrs_amd import shard
+    from ggrs_amd.p2p import PlayerType, synth_network
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    P, S, W = args.num_players, args.sessions_per_gpu, args.max_prediction
+    lo, hi = (int(x) for x in args.lag.split(","))
+    T = args.warmup + args.steps
+    mask = 0b1
+    g0, g1 = shard.shard_range(rank, world, S * world)
+    inputs, upto, rin = synth_network(g1 - g0, P, T, mask, args.remote_delay, lo, hi, seed=args.seed, first_session=g0)
+    di, du, dr = (torch.from_numpy(a).to(dev) for a in (inputs, upto, rin))
+    b = (G.SessionBuilder(G.Game.EX_GAME, num_sessions=S, device=local).with_num_players(P)
+         .with_max_prediction_window(W).with_input_delay(args.input_delay).with_remote_input_delay(args.remote_delay)
+         .with_sparse_saving_mode(args.sparse_saving).with_block_size(args.block_size))
+    for h in range(P):
+        b.add_player(PlayerType.Local if (mask >> h) & 1 else PlayerType.Remote, h)
+    sess = b.start_p2p_session()
+    stream = torch.cuda.Stream(device=dev)
+    sess.set_stream(stream)
+    tpl = args.ticks_per_launch
+
+    def run(t0, t1):
+        for t in range(t0, t1, tpl):
+            e = min(t1, t + tpl)
+            sess.run_ticks(di[t:e], du[t:e], dr)
+
+    with torch.cuda.stream(stream):
+        run(0, args.warmup)
+        torch.cuda.synchronize()
+        a0 = sess.totals()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        sess.profile_enable(True)
+        sess.profile_take()
+        t0 = time.perf_counter()
+        run(args.warmup, T)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        kernel_ms, launches = sess.profile_take()
+    a1 = sess.totals()
+    adv, saves, loads = (a1[i] - a0[i] for i in range(3))
+    thr, unexpected, panics = sess.counters()
+    tot = torch.tensor([adv, saves, loads, panics], dtype=torch.float64, device=dev)
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tot)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    adv, saves, loads, panics = (int(x) for x in tot.tolist())
+    elapsed = float(el.item())
+    if rank == 0:
+        # algorithmic bytes (this rank's launches): cells loaded + saved (40 B state,
+        # 2 B checksum, 4 B frame tag per save), the inputs of every AdvanceFrame
+        # (P bytes), and per session-tick the local input read + ring write, the
+        # delivery watermark and one remote input read + ring write (8 B)
+        state = 4 * 5 * P
+        bytes_rank = (adv / world * P + saves / world * (state + 6) + loads / world * state
+                      + S * args.steps * 8)
+        avg_kernel_s = kernel_ms / 1e3 / max(1, launches)
+        achieved = bytes_rank / max(1, launches) / avg_kernel_s / 1e9
+        line = {
+            "metric": "P2P session-frames simulated/sec (node), rollback to the first mispredicted frame",
+            "value": adv / elapsed, "unit": "session-frames/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": f"ex_game P2PSession x {S} sessions/GPU, {P} players (handle 0 local), "
+                                   f"max_prediction {W}, input delay {args.input_delay}, remote delay "
+                                   f"{args.remote_delay}, network lag {lo}-{hi} frames"
+                                   + (", sparse saving" if args.sparse_saving else ""),
+                       "sessions_per_gpu": S, "total_sessions": S * world,
+                       "advance_frames_per_session_tick": adv / (S * world * args.steps),
+                       "rollbacks_per_session_tick": loads / (S * world * args.steps),
+                       "prediction_threshold_hits": thr, "panics": panics,
+                       "parallelism": f"session-sharded x{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel_avg_us": avg_kernel_s * 1e6,
+                         "ticks_per_launch": args.steps / max(1, launches), "launches_timed": launches,
+                         "kernel": f"p2p_kernel<ExGame<{P},true>> (fused P2P ticks)"},
+            "cpu_baseline": None,
+        }
+        print(json.dumps(line), flush=True)
+    sess.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -97,7 +203,15 @@ def main():
     ap.add_argument("--cpu-ticks", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--block-size", type=int, default=0)
+    ap.add_argument("--session", choices=["synctest", "p2p"], default="synctest",
+                    help="synctest = the headline (BASELINE configs[1]); p2p = P2PSession rollback batches "
+                         "(SURVEY 8f row 1): handle 0 local, the others remote, synthetic network lag")
+    ap.add_argument("--lag", type=str, default="1,4", help="p2p: min,max network lag in frames")
+    ap.add_argument("--remote-delay", type=int, default=2, help="p2p: the remote peers' input delay")
+    ap.add_argument("--sparse-saving", action="store_true", help="p2p: with_sparse_saving_mode(true)")
     args = ap.parse_args()
+    if args.session == "p2p":
+        return bench_p2p(args)
 
     import numpy as np
     import torch

@@ -123,6 +123,7 @@ SIGNATURES = [
     ("rb_p2p_read_live", _I32, [_P, _P]),
     ("rb_p2p_state_bytes", _I32, [_P]),
     ("rb_p2p_counters", _I32, [_P, _P]),
+    ("rb_p2p_totals", _I32, [_P, _P]),
     ("rb_p2p_profile_enable", _I32, [_P, _I32]),
     ("rb_p2p_profile_take", _I32, [_P, ctypes.POINTER(ctypes.c_double), _PI32]),
 ]

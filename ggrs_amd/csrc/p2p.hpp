@@ -65,6 +65,7 @@ struct P2PParams {
   int32_t* status;          // [Spad] rb_status of the session's last advance_frame
   int32_t* trace;           // [TR_COUNT][Spad]
   uint32_t* counters;       // [0] threshold hits, [1] unexpected-path count, [2] panics
+  unsigned long long* totals;  // [0] AdvanceFrames, [1] SaveGameStates, [2] LoadGameStates executed
   const uint8_t* local_in;  // tick t, handle h: local_in + t * local_stride + (h * S + s) * IB
   int64_t local_stride;
   const int32_t* upto;      // tick t, handle h: upto[t * upto_stride + h * S + s]
@@ -171,8 +172,8 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
   const int W = p.W;
   CS* __restrict__ csa = reinterpret_cast<CS*>(p.cs);
   const RingIO<IB> ring{reinterpret_cast<uint8_t*>(p.ring), P, p.Spad};
-  auto qrow = [&](int field, int h) { return p.qs + static_cast<size_t>(QS_PLAYER0 + field * 4 + h) * Spad + s; };
-  auto player_of = [&](int j) { return kSplit ? lane : j; };
+  auto qrow = [&](int field, int h) __attribute__((always_inline)) { return p.qs + static_cast<size_t>(QS_PLAYER0 + field * 4 + h) * Spad + s; };
+  auto player_of = [&](int j) __attribute__((always_inline)) { return kSplit ? lane : j; };
 
   int32_t cur = p.qs[QS_CUR * Spad + s];
   int32_t last_saved = p.qs[QS_LAST_SAVED * Spad + s];
@@ -197,6 +198,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
 
   int32_t status = kP2PStatusOk, load_frame = kNullFrame, nadv = 0, nsave = 0;
   uint32_t nonce = 0;
+  uint32_t tot_adv = 0, tot_save = 0, tot_load = 0;  // requests the game executed in this launch
   // exec = false: bookkeeping only.  When advance_frame returns
   // Err(PredictionThreshold) the reference drops the request Vec it built
   // (p2p_session.rs:320 `?`): the sync layer has rolled back, saved and
@@ -204,7 +206,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
   // reproduces that bookkeeping without touching the game state or the cells.
   bool exec = true;
   // SaveGameState{cell, frame}: game checksum, cell.save (sync_layer.rs:118-125)
-  auto save = [&](int32_t f) {
+  auto save = [&](int32_t f) __attribute__((always_inline)) {
     last_saved = f;
     ++nsave;
     if (!exec) return;
@@ -218,7 +220,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     }
   };
   // SyncLayer::synchronized_inputs (sync_layer.rs:187-200) for this lane's players
-  auto sync_inputs = [&](int32_t f) -> InRec {
+  auto sync_inputs = [&](int32_t f) __attribute__((always_inline)) -> InRec {
     uint64_t rec = 0;
 #pragma unroll
     for (int j = 0; j < PPL; ++j) {
@@ -227,13 +229,13 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     }
     return static_cast<InRec>(rec);
   };
-  auto advance = [&](int32_t f) {  // AdvanceFrame{inputs}
+  auto advance = [&](int32_t f) __attribute__((always_inline)) {  // AdvanceFrame{inputs}
     const InRec rec = sync_inputs(f);
     ++nadv;
     if (exec) G::advance(w, rec, lane, 0u, &p.counters[1]);
   };
   // P2PSession::adjust_gamestate (p2p_session.rs:621-673)
-  auto adjust = [&](int32_t first_incorrect, int32_t min_confirmed) {
+  auto adjust = [&](int32_t first_incorrect, int32_t min_confirmed) __attribute__((always_inline)) {
     const int32_t to_load = p.sparse ? last_saved : first_incorrect;
     const int32_t count = cur - to_load;
     const unsigned slot = static_cast<unsigned>(to_load % W);
@@ -258,7 +260,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
   };
   // advance_frame (p2p_session.rs:253-303) up to the local inputs: frame-0
   // save, rollback, save / sparse check, set_last_confirmed_frame.
-  auto rollback_and_save = [&]() {
+  auto rollback_and_save = [&]() __attribute__((always_inline)) {
     load_frame = kNullFrame;
     nadv = nsave = 0;
     if (cur == 0) save(cur);
@@ -339,6 +341,8 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     }
     rollback_and_save();
     if (status == kP2PStatusPanic) break;
+    tot_save += static_cast<uint32_t>(nsave);
+    tot_load += load_frame != kNullFrame;
     // ---- local inputs: SyncLayer::add_local_input (sync_layer.rs:159-174)
 #pragma unroll
     for (int j = 0; j < PPL; ++j) {
@@ -351,6 +355,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     }
     advance(cur);
     cur += 1;
+    tot_adv += static_cast<uint32_t>(nadv);
   }
 
   // ---- write back
@@ -375,6 +380,9 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     p.trace[TR_NADV * Spad + s] = nadv;
     p.trace[TR_NSAVE * Spad + s] = nsave;
     if (status == kP2PStatusPanic) atomicAdd(&p.counters[2], 1u);
+    atomicAdd(&p.totals[0], static_cast<unsigned long long>(tot_adv));
+    atomicAdd(&p.totals[1], static_cast<unsigned long long>(tot_save));
+    atomicAdd(&p.totals[2], static_cast<unsigned long long>(tot_load));
   }
 }
 

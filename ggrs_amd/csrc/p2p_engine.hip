@@ -24,6 +24,7 @@ struct rb_p2p {
   int32_t* status = nullptr;
   int32_t* trace = nullptr;
   uint32_t* counters = nullptr;
+  unsigned long long* totals = nullptr;
   bool prof = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev;
   size_t prof_used = 0;
@@ -47,7 +48,7 @@ rb_status pfail(rb_p2p* b, rb_status st, const std::string& msg) {
 void free_all(rb_p2p* b) {
   (void)hipSetDevice(b->device);
   if (b->stream) (void)hipStreamSynchronize(b->stream);
-  void* ptrs[] = {b->snap, b->cs, b->tag, b->ring, b->live, b->qs, b->status, b->trace, b->counters};
+  void* ptrs[] = {b->snap, b->cs, b->tag, b->ring, b->live, b->qs, b->status, b->trace, b->counters, b->totals};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   for (auto& pr : b->prof_ev) {
@@ -152,6 +153,7 @@ rb_status rb_p2p_create(const rb_p2p_config* cfg, rb_p2p** out) {
   P2P_CREATE(hipMalloc(&b->status, Sp * 4));
   P2P_CREATE(hipMalloc(&b->trace, TR_COUNT * Sp * 4));
   P2P_CREATE(hipMalloc(&b->counters, 16));
+  P2P_CREATE(hipMalloc(&b->totals, 32));
   P2P_CREATE(hipMemsetAsync(b->snap, 0, W * NW * Gp * 4, b->stream));
   P2P_CREATE(hipMemsetAsync(b->cs, 0, W * Sp * b->ops->cs_bytes, b->stream));
   P2P_CREATE(hipMemsetAsync(b->tag, 0xff, W * Sp * 4, b->stream));  // GameState::default frame = NULL_FRAME
@@ -159,6 +161,7 @@ rb_status rb_p2p_create(const rb_p2p_config* cfg, rb_p2p** out) {
   P2P_CREATE(hipMemsetAsync(b->status, 0, Sp * 4, b->stream));
   P2P_CREATE(hipMemsetAsync(b->trace, 0xff, TR_COUNT * Sp * 4, b->stream));
   P2P_CREATE(hipMemsetAsync(b->counters, 0, 16, b->stream));
+  P2P_CREATE(hipMemsetAsync(b->totals, 0, 32, b->stream));
   // SyncLayer::new / InputQueue::new / ConnectionStatus::default: every frame NULL, current 0
   std::vector<int32_t> qs(kQsFields * Sp, kNullFrame);
   for (size_t s = 0; s < Sp; ++s) {
@@ -210,6 +213,7 @@ rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs,
   p.status = b->status;
   p.trace = b->trace;
   p.counters = b->counters;
+  p.totals = b->totals;
   p.local_in = static_cast<const uint8_t*>(local_inputs);
   p.local_stride = local_stride;
   p.upto = remote_upto;
@@ -312,6 +316,14 @@ rb_status rb_p2p_counters(rb_p2p* b, uint32_t* out3) {
   uint32_t c[4];
   P2P_TRY(b, hipStreamSynchronize(b->stream));
   P2P_TRY(b, hipMemcpy(c, b->counters, 16, hipMemcpyDeviceToHost));
+  for (int i = 0; i < 3; ++i) out3[i] = c[i];
+  return RB_OK;
+}
+
+rb_status rb_p2p_totals(rb_p2p* b, uint64_t* out3) {
+  unsigned long long c[4];
+  P2P_TRY(b, hipStreamSynchronize(b->stream));
+  P2P_TRY(b, hipMemcpy(c, b->totals, 32, hipMemcpyDeviceToHost));
   for (int i = 0; i < 3; ++i) out3[i] = c[i];
   return RB_OK;
 }

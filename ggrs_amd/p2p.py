@@ -138,6 +138,12 @@ class P2PSession:
         self._check(self._lib.rb_p2p_counters(self._h, c))
         return tuple(c)
 
+    def totals(self):
+        """(AdvanceFrames, SaveGameStates, LoadGameStates) the games executed since create."""
+        c = (ctypes.c_uint64 * 3)()
+        self._check(self._lib.rb_p2p_totals(self._h, c))
+        return tuple(int(x) for x in c)
+
     def profile_enable(self, on: bool) -> None:
         self._check(self._lib.rb_p2p_profile_enable(self._h, int(on)))
 

@@ -267,6 +267,9 @@ rb_status rb_p2p_read_live(rb_p2p* b, void* images);
 int32_t rb_p2p_state_bytes(const rb_p2p* b);
 /* Counters since create: [0] PredictionThreshold hits, [1] unexpected math paths, [2] panicked sessions. */
 rb_status rb_p2p_counters(rb_p2p* b, uint32_t* out3);
+/* Requests the games executed since create: [0] AdvanceFrame, [1] SaveGameState,
+ * [2] LoadGameState (requests dropped with a PredictionThreshold error excluded). */
+rb_status rb_p2p_totals(rb_p2p* b, uint64_t* out3);
 /* HIP event timing of every rb_p2p_run_ticks launch (bench.py): total ms and launches since the last take. */
 rb_status rb_p2p_profile_enable(rb_p2p* b, int32_t on);
 rb_status rb_p2p_profile_take(rb_p2p* b, double* total_ms, int32_t* launches);
