@@ -35,6 +35,7 @@ RB_GAME_BRAWLER = 5
 
 RB_FLAG_CHECKED = 1
 RB_FLAG_LANE_PER_SESSION = 2
+RB_P2P_FLAG_FANOUT = 4
 
 
 class RbConfig(ctypes.Structure):

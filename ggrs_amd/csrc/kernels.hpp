@@ -537,8 +537,11 @@ struct GameOps {
   bool launch_steady_supported(int cd) const { return cd >= 1 && cd <= 8; }
   virtual hipError_t launch_report(const void* cs, const int32_t* err, int S, int32_t frame, void* out,
                                    hipStream_t st) const = 0;
-  // P2PSession ticks (p2p.hpp)
+  // P2PSession ticks and the speculative fan-out (p2p.hpp); fan-out needs one
+  // lane per player (ex_game), hipErrorNotSupported otherwise
   virtual hipError_t launch_p2p(const P2PParams& p, int block, hipStream_t st) const = 0;
+  virtual hipError_t launch_fanout(const FanParams& p, int block, hipStream_t st) const = 0;
+  bool fanout_supported = false;
 };
 
 template <class G>
@@ -553,6 +556,7 @@ struct GameOpsT final : GameOps {
     cs_bytes = sizeof(typename G::CS);
     image_bytes = G::kImageBytes;
     display = G::kDisplay;
+    fanout_supported = kFanout;
   }
   void word_loc(int k, int* lane, int* word) const override { G::word_loc(k, lane, word); }
   void init_words(uint32_t* w) const override { G::init(w); }
@@ -606,6 +610,16 @@ struct GameOpsT final : GameOps {
     const int grid = (p.Spad * G::kLanes + block - 1) / block;
     hipLaunchKernelGGL(p2p_kernel<G>, dim3(grid), dim3(block), 0, st, p);
     return hipGetLastError();
+  }
+  static constexpr bool kFanout = G::kLanes > 1 && G::kLanes <= 4;
+  hipError_t launch_fanout(const FanParams& p, int block, hipStream_t st) const override {
+    if constexpr (kFanout) {
+      const int grid = (p.Spad * kSpecBranches * G::kLanes + block - 1) / block;
+      hipLaunchKernelGGL(fanout_kernel<G>, dim3(grid), dim3(block), 0, st, p);
+      return hipGetLastError();
+    } else {
+      return hipErrorNotSupported;
+    }
   }
 };
 

@@ -54,6 +54,12 @@ constexpr int kQsFields = QS_PLAYER0 + QF_COUNT * 4;
 // trace rows (the last tick of the last launch): LoadGameState frame, AdvanceFrame count, SaveGameState count
 enum : int { TR_LOAD = 0, TR_NADV = 1, TR_NSAVE = 2, TR_COUNT = 3 };
 constexpr int32_t kP2PStatusOk = 0, kP2PStatusThreshold = 1, kP2PStatusPanic = 101;
+// Speculative fan-out: branch k holds candidate input k for one remote player
+// over its unconfirmed frames (the full 4-bit ex_game alphabet).
+constexpr int kSpecBranches = 16;
+// spec_meta rows: first speculated frame (base), frame the branch states are at
+// (end), speculated handle, valid flag
+enum : int { SM_BASE = 0, SM_END = 1, SM_PLAYER = 2, SM_VALID = 3, SM_COUNT = 4 };
 
 struct P2PParams {
   uint32_t* snap;
@@ -65,7 +71,14 @@ struct P2PParams {
   int32_t* status;          // [Spad] rb_status of the session's last advance_frame
   int32_t* trace;           // [TR_COUNT][Spad]
   uint32_t* counters;       // [0] threshold hits, [1] unexpected-path count, [2] panics
-  unsigned long long* totals;  // [0] AdvanceFrames, [1] SaveGameStates, [2] LoadGameStates executed
+  unsigned long long* totals;  // executed: [0] AdvanceFrames, [1] SaveGameStates, [2] LoadGameStates,
+                               // [3] rollbacks replaced by a speculative branch select, [4] branch frames presimulated
+  // speculative fan-out (fanout_kernel below; spec_on = 0: plain P2P)
+  const uint32_t* spec_state;  // [kSpecBranches][NW planes][Spad*L] branch states at meta end
+  const uint32_t* spec_cells;  // [W][kSpecBranches][NW planes][Spad*L] branch cells
+  const void* spec_cs;         // [W][kSpecBranches][Spad] CS
+  const int32_t* spec_meta;    // [SM_COUNT][Spad]
+  int32_t spec_on;
   const uint8_t* local_in;  // tick t, handle h: local_in + t * local_stride + (h * S + s) * IB
   int64_t local_stride;
   const int32_t* upto;      // tick t, handle h: upto[t * upto_stride + h * S + s]
@@ -198,7 +211,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
 
   int32_t status = kP2PStatusOk, load_frame = kNullFrame, nadv = 0, nsave = 0;
   uint32_t nonce = 0;
-  uint32_t tot_adv = 0, tot_save = 0, tot_load = 0;  // requests the game executed in this launch
+  uint32_t tot_adv = 0, tot_save = 0, tot_load = 0, tot_sel = 0;  // requests the game executed in this launch
   // exec = false: bookkeeping only.  When advance_frame returns
   // Err(PredictionThreshold) the reference drops the request Vec it built
   // (p2p_session.rs:320 `?`): the sync layer has rolled back, saved and
@@ -210,6 +223,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     last_saved = f;
     ++nsave;
     if (!exec) return;
+    ++tot_save;
     CsCtx ctx{0ull, s, nonce++};
     const CS c = G::checksum(w, f, lane, ctx);
     const unsigned slot = static_cast<unsigned>(f % W);
@@ -232,7 +246,10 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
   auto advance = [&](int32_t f) __attribute__((always_inline)) {  // AdvanceFrame{inputs}
     const InRec rec = sync_inputs(f);
     ++nadv;
-    if (exec) G::advance(w, rec, lane, 0u, &p.counters[1]);
+    if (exec) {
+      G::advance(w, rec, lane, 0u, &p.counters[1]);
+      ++tot_adv;
+    }
   };
   // P2PSession::adjust_gamestate (p2p_session.rs:621-673)
   auto adjust = [&](int32_t first_incorrect, int32_t min_confirmed) __attribute__((always_inline)) {
@@ -243,7 +260,10 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
       status = kP2PStatusPanic;  // a reference assert (sync_layer.rs:141-148) would fire
       return;
     }
-    if (exec) load_words<NW>(p.snap + slot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), w);  // LoadGameState
+    if (exec) {  // LoadGameState
+      load_words<NW>(p.snap + slot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), w);
+      ++tot_load;
+    }
     load_frame = to_load;
     cur = to_load;
 #pragma unroll
@@ -257,6 +277,59 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
       advance(cur);
       cur += 1;
     }
+  };
+  // Speculative select: when the only misprediction is the speculated
+  // player's, starting exactly at the branch base, and every input it
+  // confirmed since is one value k held, branch k (fanout_kernel, previous
+  // tick) already holds what adjust_gamestate would recompute: the states of
+  // frames base+1 .. cur-1 and of frame cur, built from the same inputs (k
+  // confirmed then k predicted for the speculated player, the reference's
+  // predictions for the others, confirmed local inputs).  The sync layer's
+  // bookkeeping runs as in adjust (dry), the cells and the state are copied.
+  auto try_select = [&](int32_t first_incorrect, int32_t min_confirmed) __attribute__((always_inline)) -> bool {
+    if (!p.spec_meta[SM_VALID * Spad + s] || p.spec_meta[SM_END * Spad + s] != cur) return false;
+    const int32_t base = p.spec_meta[SM_BASE * Spad + s];
+    const int rs = p.spec_meta[SM_PLAYER * Spad + s];
+    if (first_incorrect != base || base + W <= cur) return false;
+    // every mispredicting player must be the speculated one; its confirmed run from base must be one value
+    bool ok = true;
+    uint32_t k = 0;
+#pragma unroll
+    for (int j = 0; j < PPL; ++j) {
+      const int h = player_of(j);
+      if (h >= P) continue;
+      if (h != rs) {
+        ok &= q[j].first_inc == kNullFrame;
+      } else {
+        k = ring.get(base, h, s);
+        for (int32_t f = base + 1; f <= q[j].last_added && f < cur; ++f) ok &= ring.get(f, h, s) == k;
+      }
+    }
+    // the lane that owns the speculated player found k; share it with the group
+    int32_t kk = (kSplit ? lane == rs : true) ? static_cast<int32_t>(k) : -1;
+    kk = -group_min<L>(-kk);  // max over the group
+    ok = group_min<L>(ok ? 1 : 0) == 1;
+    if (!ok || kk < 0 || kk >= kSpecBranches) return false;
+    exec = false;  // the sync layer's side of adjust_gamestate
+    adjust(first_incorrect, min_confirmed);
+    exec = true;
+    if (status == kP2PStatusPanic) return true;
+    const unsigned bw = static_cast<unsigned>(NW) * Gpad;  // words of one branch block
+    const CS* __restrict__ scs = reinterpret_cast<const CS*>(p.spec_cs);
+    for (int32_t f = base + 1; f < cur; ++f) {  // the cells adjust would have saved
+      const unsigned slot = static_cast<unsigned>(f % W);
+      uint32_t cw[NW];
+      load_words<NW>(p.spec_cells + (slot * kSpecBranches + kk) * bw, static_cast<int>(Gpad), static_cast<int>(g), cw);
+      store_words<NW>(p.snap + slot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), cw);
+      if (lead) {
+        csa[slot * Spad + s] = scs[(slot * kSpecBranches + kk) * Spad + s];
+        p.tag[slot * Spad + s] = f;
+      }
+      ++tot_save;
+    }
+    load_words<NW>(p.spec_state + kk * bw, static_cast<int>(Gpad), static_cast<int>(g), w);
+    ++tot_sel;
+    return true;
   };
   // advance_frame (p2p_session.rs:253-303) up to the local inputs: frame-0
   // save, rollback, save / sparse check, set_last_confirmed_frame.
@@ -272,7 +345,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     }
     confirmed = group_min<L>(confirmed);
     first_inc = group_min<L>(first_inc);
-    if (first_inc != INT32_MAX) adjust(first_inc, confirmed);
+    if (first_inc != INT32_MAX && !(p.spec_on && exec && try_select(first_inc, confirmed))) adjust(first_inc, confirmed);
     if (status == kP2PStatusPanic) return;
     if (p.sparse) {  // check_last_saved_state (:778-802)
       if (cur - last_saved >= W) {
@@ -341,8 +414,6 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     }
     rollback_and_save();
     if (status == kP2PStatusPanic) break;
-    tot_save += static_cast<uint32_t>(nsave);
-    tot_load += load_frame != kNullFrame;
     // ---- local inputs: SyncLayer::add_local_input (sync_layer.rs:159-174)
 #pragma unroll
     for (int j = 0; j < PPL; ++j) {
@@ -355,7 +426,6 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     }
     advance(cur);
     cur += 1;
-    tot_adv += static_cast<uint32_t>(nadv);
   }
 
   // ---- write back
@@ -383,7 +453,112 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     atomicAdd(&p.totals[0], static_cast<unsigned long long>(tot_adv));
     atomicAdd(&p.totals[1], static_cast<unsigned long long>(tot_save));
     atomicAdd(&p.totals[2], static_cast<unsigned long long>(tot_load));
+    if (tot_sel) atomicAdd(&p.totals[3], static_cast<unsigned long long>(tot_sel));
   }
+}
+
+// ---------------------------------------------------------------------------
+// Speculative branch fan-out (BASELINE config 4).  After a
+// tick, for every session: take the remote handle with the oldest unconfirmed
+// input (the speculated player), its first unconfirmed frame `base`, and
+// presimulate kSpecBranches branches from the saved cell of `base` up to the
+// current frame: branch k feeds candidate k to the speculated player on every
+// frame of the window and, for everybody else, exactly the inputs a rollback
+// would use (confirmed inputs, the reference's repeat-last predictions).  Each
+// branch saves its cells like adjust_gamestate would.  One lane group (a
+// branch) per candidate, one lane per player: 16 x L lanes per session, all
+// branches in lock-step.  The next tick's p2p_kernel turns a matching
+// misprediction into a select (try_select) instead of a resimulation.
+// ---------------------------------------------------------------------------
+struct FanParams {
+  const uint32_t* snap;
+  const int32_t* tag;
+  const void* ring;
+  const int32_t* qs;
+  uint32_t* spec_state;
+  uint32_t* spec_cells;
+  void* spec_cs;
+  int32_t* spec_meta;
+  unsigned long long* totals;
+  uint32_t* counters;
+  int32_t S, Spad, W;
+  uint32_t local_mask;
+};
+
+template <class G>
+__global__ void __launch_bounds__(256) fanout_kernel(const FanParams p) {
+  using InRec = typename G::InRec;
+  using CS = typename G::CS;
+  constexpr int NW = G::NWL;
+  constexpr int L = G::kLanes;
+  constexpr int P = G::kPlayers, IB = G::kInputBytes;
+  static_assert(L > 1 || P == 1, "fan-out runs with one lane per player");
+  constexpr int LS = kSpecBranches * L;  // lanes per session
+  const unsigned g = blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned s = g / LS;
+  const int r = static_cast<int>(g % LS);
+  const int k = r / L, lane = r % L;  // branch = candidate input, player slot
+  if (s >= static_cast<unsigned>(p.S)) return;
+  const unsigned Spad = static_cast<unsigned>(p.Spad), Gpad = Spad * L;
+  const unsigned bw = static_cast<unsigned>(NW) * Gpad;
+  const int W = p.W;
+  const RingIO<IB> ring{const_cast<uint8_t*>(reinterpret_cast<const uint8_t*>(p.ring)), P, p.Spad};
+  auto qrow = [&](int field, int h) { return p.qs[static_cast<size_t>(QS_PLAYER0 + field * 4 + h) * Spad + s]; };
+  const int32_t cur = p.qs[QS_CUR * Spad + s];
+  // the remote handle with the oldest last added input (ties: lowest handle)
+  int rs = -1;
+  int32_t la_rs = INT32_MAX;
+#pragma unroll
+  for (int h = 0; h < P; ++h) {
+    if ((p.local_mask >> h) & 1u) continue;
+    const int32_t la = qrow(QF_LAST_ADDED, h);
+    const int32_t key = la == kNullFrame ? -1 : la;
+    if (key < la_rs) {
+      la_rs = key;
+      rs = h;
+    }
+  }
+  const int32_t base = la_rs + 1;  // first unconfirmed frame of the speculated player
+  const bool valid = rs >= 0 && base < cur && base + W > cur && base >= 0 &&
+                     p.tag[static_cast<unsigned>(base % W) * Spad + s] == base;
+  if (k == 0 && lane == 0) {
+    p.spec_meta[SM_BASE * Spad + s] = base;
+    p.spec_meta[SM_END * Spad + s] = cur;
+    p.spec_meta[SM_PLAYER * Spad + s] = rs;
+    p.spec_meta[SM_VALID * Spad + s] = valid ? 1 : 0;
+  }
+  if (!valid) return;  // session-uniform: the whole group leaves
+  const unsigned gl = s * L + lane;  // this lane's column in the session-major planes
+  uint32_t w[NW];
+  load_words<NW>(p.snap + static_cast<unsigned>(base % W) * bw, static_cast<int>(Gpad), static_cast<int>(gl), w);
+  // this lane's player: its inputs over the window, as adjust_gamestate would see them
+  const int h = lane;
+  const bool active = h < P;
+  const bool local = active && ((p.local_mask >> h) & 1u);
+  const int32_t la_h = active ? qrow(QF_LAST_ADDED, h) : kNullFrame;
+  const uint32_t pred = (!active || la_h == kNullFrame) ? 0u : ring.get(la_h, h, s);
+  CS* __restrict__ cs = reinterpret_cast<CS*>(p.spec_cs);
+  uint32_t frames = 0;
+  for (int32_t f = base; f < cur; ++f) {
+    if (f > base) {  // SaveGameState of frame f (adjust_gamestate saves every frame but the loaded one)
+      CsCtx ctx{0ull, s, 0u};
+      const CS c = G::checksum(w, f, lane, ctx);
+      const unsigned slot = static_cast<unsigned>(f % W);
+      store_words<NW>(p.spec_cells + (slot * kSpecBranches + k) * bw, static_cast<int>(Gpad), static_cast<int>(gl), w);
+      if (lane == 0) cs[(slot * kSpecBranches + k) * Spad + s] = c;
+    }
+    uint32_t v = 0;
+    if (active) {
+      if (h == rs) v = static_cast<uint32_t>(k);
+      else if (local || (la_h != kNullFrame && f <= la_h)) v = ring.get(f, h, s);  // Confirmed
+      else v = pred;  // repeat-last prediction (blank before the first input)
+    }
+    G::advance(w, static_cast<InRec>(static_cast<uint64_t>(v) << (8 * IB * (active ? h : 0))), lane, 0u,
+               &p.counters[1]);
+    ++frames;
+  }
+  store_words<NW>(p.spec_state + k * bw, static_cast<int>(Gpad), static_cast<int>(gl), w);
+  if (lane == 0) atomicAdd(&p.totals[4], static_cast<unsigned long long>(frames));
 }
 
 }  // namespace rb

@@ -25,6 +25,11 @@ struct rb_p2p {
   int32_t* trace = nullptr;
   uint32_t* counters = nullptr;
   unsigned long long* totals = nullptr;
+  bool fanout = false;
+  uint32_t* spec_state = nullptr;
+  uint32_t* spec_cells = nullptr;
+  void* spec_cs = nullptr;
+  int32_t* spec_meta = nullptr;
   bool prof = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev;
   size_t prof_used = 0;
@@ -48,7 +53,8 @@ rb_status pfail(rb_p2p* b, rb_status st, const std::string& msg) {
 void free_all(rb_p2p* b) {
   (void)hipSetDevice(b->device);
   if (b->stream) (void)hipStreamSynchronize(b->stream);
-  void* ptrs[] = {b->snap, b->cs, b->tag, b->ring, b->live, b->qs, b->status, b->trace, b->counters, b->totals};
+  void* ptrs[] = {b->snap,   b->cs,      b->tag,       b->ring,       b->live,    b->qs,       b->status,
+                  b->trace,  b->counters, b->totals, b->spec_state, b->spec_cells, b->spec_cs, b->spec_meta};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   for (auto& pr : b->prof_ev) {
@@ -114,6 +120,9 @@ rb_status rb_p2p_create(const rb_p2p_config* cfg, rb_p2p** out) {
     return pfail(nullptr, RB_INVALID_REQUEST, "P2P batches support ex_game, the stub game and the brawler");
   auto ops = make_game(cfg->game, cfg->num_players, (cfg->flags & RB_FLAG_LANE_PER_SESSION) != 0);
   if (!ops) return pfail(nullptr, RB_INVALID_REQUEST, "unsupported game / num_players combination");
+  const bool fanout = (cfg->flags & RB_P2P_FLAG_FANOUT) != 0;
+  if (fanout && (!ops->fanout_supported || cfg->sparse_saving))
+    return pfail(nullptr, RB_INVALID_REQUEST, "speculative fan-out needs ex_game with one lane per player, no sparse saving");
   if (static_cast<uint64_t>(cfg->max_prediction) * ops->nw * ops->lanes *
           ((static_cast<uint64_t>(cfg->num_sessions) + 63) / 64 * 64) >= (1ull << 32))
     return pfail(nullptr, RB_INVALID_REQUEST, "batch too large for 32-bit snapshot offsets");
@@ -128,6 +137,7 @@ rb_status rb_p2p_create(const rb_p2p_config* cfg, rb_p2p** out) {
   b->block = cfg->block_size ? static_cast<int>(cfg->block_size) : 256;
   if (b->block % 64 != 0 || b->block > 256) return pfail(nullptr, RB_INVALID_REQUEST, "block_size must be 64, 128, 192 or 256");
   b->device = cfg->device;
+  b->fanout = fanout;
   rb_p2p* bp = b.get();
   auto hip_fail = [&](hipError_t e, const char* what) {
     g_p2p_err = std::string(what) + ": " + hipGetErrorString(e);
@@ -153,7 +163,7 @@ rb_status rb_p2p_create(const rb_p2p_config* cfg, rb_p2p** out) {
   P2P_CREATE(hipMalloc(&b->status, Sp * 4));
   P2P_CREATE(hipMalloc(&b->trace, TR_COUNT * Sp * 4));
   P2P_CREATE(hipMalloc(&b->counters, 16));
-  P2P_CREATE(hipMalloc(&b->totals, 32));
+  P2P_CREATE(hipMalloc(&b->totals, 64));
   P2P_CREATE(hipMemsetAsync(b->snap, 0, W * NW * Gp * 4, b->stream));
   P2P_CREATE(hipMemsetAsync(b->cs, 0, W * Sp * b->ops->cs_bytes, b->stream));
   P2P_CREATE(hipMemsetAsync(b->tag, 0xff, W * Sp * 4, b->stream));  // GameState::default frame = NULL_FRAME
@@ -161,7 +171,15 @@ rb_status rb_p2p_create(const rb_p2p_config* cfg, rb_p2p** out) {
   P2P_CREATE(hipMemsetAsync(b->status, 0, Sp * 4, b->stream));
   P2P_CREATE(hipMemsetAsync(b->trace, 0xff, TR_COUNT * Sp * 4, b->stream));
   P2P_CREATE(hipMemsetAsync(b->counters, 0, 16, b->stream));
-  P2P_CREATE(hipMemsetAsync(b->totals, 0, 32, b->stream));
+  P2P_CREATE(hipMemsetAsync(b->totals, 0, 64, b->stream));
+  if (b->fanout) {
+    const size_t K = kSpecBranches;
+    P2P_CREATE(hipMalloc(&b->spec_state, K * NW * Gp * 4));
+    P2P_CREATE(hipMalloc(&b->spec_cells, W * K * NW * Gp * 4));
+    P2P_CREATE(hipMalloc(&b->spec_cs, W * K * Sp * b->ops->cs_bytes));
+    P2P_CREATE(hipMalloc(&b->spec_meta, SM_COUNT * Sp * 4));
+    P2P_CREATE(hipMemsetAsync(b->spec_meta, 0, SM_COUNT * Sp * 4, b->stream));  // nothing valid yet
+  }
   // SyncLayer::new / InputQueue::new / ConnectionStatus::default: every frame NULL, current 0
   std::vector<int32_t> qs(kQsFields * Sp, kNullFrame);
   for (size_t s = 0; s < Sp; ++s) {
@@ -228,6 +246,26 @@ rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs,
   p.T = n_ticks;
   p.local_mask = b->cfg.local_mask;
   p.sparse = b->cfg.sparse_saving != 0;
+  p.spec_on = b->fanout ? 1 : 0;
+  p.spec_state = b->spec_state;
+  p.spec_cells = b->spec_cells;
+  p.spec_cs = b->spec_cs;
+  p.spec_meta = b->spec_meta;
+  FanParams fp{};
+  fp.snap = b->snap;
+  fp.tag = b->tag;
+  fp.ring = b->ring;
+  fp.qs = b->qs;
+  fp.spec_state = b->spec_state;
+  fp.spec_cells = b->spec_cells;
+  fp.spec_cs = b->spec_cs;
+  fp.spec_meta = b->spec_meta;
+  fp.totals = b->totals;
+  fp.counters = b->counters;
+  fp.S = b->S;
+  fp.Spad = b->Spad;
+  fp.W = b->W;
+  fp.local_mask = b->cfg.local_mask;
   P2P_TRY(b, hipSetDevice(b->device));
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (b->prof) {
@@ -241,7 +279,21 @@ rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs,
     ++b->prof_used;
     P2P_TRY(b, hipEventRecord(e0, b->stream));
   }
-  hipError_t e = b->ops->launch_p2p(p, b->block, b->stream);
+  hipError_t e = hipSuccess;
+  if (!b->fanout) {
+    e = b->ops->launch_p2p(p, b->block, b->stream);  // all ticks in one launch
+  } else {
+    // the fan-out between ticks needs every lane of a session's branches: one
+    // P2P launch and one fan-out launch per tick
+    P2PParams pt = p;
+    pt.T = 1;
+    for (int32_t t = 0; t < n_ticks && e == hipSuccess; ++t) {
+      pt.local_in = p.local_in + static_cast<int64_t>(t) * p.local_stride;
+      pt.upto = p.upto + static_cast<int64_t>(t) * p.upto_stride;
+      e = b->ops->launch_p2p(pt, b->block, b->stream);
+      if (e == hipSuccess) e = b->ops->launch_fanout(fp, b->block, b->stream);
+    }
+  }
   if (e != hipSuccess) return pfail(b, RB_DEVICE_ERROR, std::string("p2p launch: ") + hipGetErrorString(e));
   if (b->prof) P2P_TRY(b, hipEventRecord(e1, b->stream));
   return RB_OK;
@@ -320,11 +372,11 @@ rb_status rb_p2p_counters(rb_p2p* b, uint32_t* out3) {
   return RB_OK;
 }
 
-rb_status rb_p2p_totals(rb_p2p* b, uint64_t* out3) {
-  unsigned long long c[4];
+rb_status rb_p2p_totals(rb_p2p* b, uint64_t* out5) {
+  unsigned long long c[8];
   P2P_TRY(b, hipStreamSynchronize(b->stream));
-  P2P_TRY(b, hipMemcpy(c, b->totals, 32, hipMemcpyDeviceToHost));
-  for (int i = 0; i < 3; ++i) out3[i] = c[i];
+  P2P_TRY(b, hipMemcpy(c, b->totals, 64, hipMemcpyDeviceToHost));
+  for (int i = 0; i < 5; ++i) out5[i] = c[i];
   return RB_OK;
 }
 

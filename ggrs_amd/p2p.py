@@ -139,8 +139,9 @@ class P2PSession:
         return tuple(c)
 
     def totals(self):
-        """(AdvanceFrames, SaveGameStates, LoadGameStates) the games executed since create."""
-        c = (ctypes.c_uint64 * 3)()
+        """Work executed since create: (AdvanceFrames, SaveGameStates, LoadGameStates,
+        speculative selects, branch frames presimulated)."""
+        c = (ctypes.c_uint64 * 5)()
         self._check(self._lib.rb_p2p_totals(self._h, c))
         return tuple(int(x) for x in c)
 

@@ -232,6 +232,12 @@ class SessionBuilder:
         self._sparse = bool(sparse_saving)
         return self
 
+    def with_speculative_fanout(self, on: bool) -> "SessionBuilder":
+        """P2P: presimulate 16 candidate inputs of the most-lagging remote handle
+        after every tick (RB_P2P_FLAG_FANOUT, BASELINE config 4)."""
+        self._fanout = bool(on)
+        return self
+
     def with_remote_input_delay(self, delay: int) -> "SessionBuilder":
         """Frame of each remote handle's first input (the peers' input delay)."""
         self._remote_delay = int(delay)
@@ -260,7 +266,8 @@ class SessionBuilder:
         pc.local_mask = sum(1 << h for h, t in players.items() if t == PlayerType.Local)
         pc.remote_delay = getattr(self, "_remote_delay", 0)
         pc.sparse_saving = int(getattr(self, "_sparse", False))
-        pc.flags = self._cfg.flags & L.RB_FLAG_LANE_PER_SESSION
+        pc.flags = (self._cfg.flags & L.RB_FLAG_LANE_PER_SESSION) | (
+            L.RB_P2P_FLAG_FANOUT if getattr(self, "_fanout", False) else 0)
         pc.block_size = self._cfg.block_size
         h = ctypes.c_void_p()
         st = lib.rb_p2p_create(ctypes.byref(pc), ctypes.byref(h))

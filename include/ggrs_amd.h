@@ -222,10 +222,19 @@ typedef struct rb_p2p_config {
   uint32_t local_mask;    /* bit h: handle h is PlayerType::Local; at least one local and one remote */
   int32_t remote_delay;   /* frame of each remote handle's first Event::Input (the peer's input delay) */
   int32_t sparse_saving;  /* with_sparse_saving_mode (builder.rs:159-166) */
-  uint32_t flags;         /* RB_FLAG_LANE_PER_SESSION only */
+  uint32_t flags;         /* RB_FLAG_LANE_PER_SESSION, RB_P2P_FLAG_FANOUT */
   uint32_t block_size;
   uint32_t reserved[4];
 } rb_p2p_config;
+
+/* Speculative branch fan-out (BASELINE config 4): after every tick each session
+ * presimulates 16 branches, one per candidate input (the 4-bit ex_game
+ * alphabet) of the remote handle with the oldest unconfirmed input, over its
+ * unconfirmed frames.  A later misprediction of that handle alone, held at
+ * one value, becomes a branch select instead of LoadGameState + resimulation;
+ * cells, states, statuses and frames stay identical to the plain rollback.
+ * ex_game with one lane per player only; not with sparse saving. */
+#define RB_P2P_FLAG_FANOUT 4u
 
 /* SessionBuilder::new() defaults for a 2-player session, handle 0 local, handle 1 remote. */
 void rb_p2p_config_init(rb_p2p_config* cfg);
@@ -267,9 +276,11 @@ rb_status rb_p2p_read_live(rb_p2p* b, void* images);
 int32_t rb_p2p_state_bytes(const rb_p2p* b);
 /* Counters since create: [0] PredictionThreshold hits, [1] unexpected math paths, [2] panicked sessions. */
 rb_status rb_p2p_counters(rb_p2p* b, uint32_t* out3);
-/* Requests the games executed since create: [0] AdvanceFrame, [1] SaveGameState,
- * [2] LoadGameState (requests dropped with a PredictionThreshold error excluded). */
-rb_status rb_p2p_totals(rb_p2p* b, uint64_t* out3);
+/* Work the device executed since create: [0] AdvanceFrame, [1] SaveGameState,
+ * [2] LoadGameState (requests dropped with a PredictionThreshold error
+ * excluded), [3] rollbacks replaced by a speculative select, [4] branch frames
+ * presimulated by the fan-out. */
+rb_status rb_p2p_totals(rb_p2p* b, uint64_t* out5);
 /* HIP event timing of every rb_p2p_run_ticks launch (bench.py): total ms and launches since the last take. */
 rb_status rb_p2p_profile_enable(rb_p2p* b, int32_t on);
 rb_status rb_p2p_profile_take(rb_p2p* b, double* total_ms, int32_t* launches);

@@ -116,10 +116,10 @@ def test_oracle_prediction_threshold_drops_the_requests():
 
 
 # ---------------------------------------------------------------------------- device vs oracle
-def gpu_pair(game, S, P, W, d, rd, mask, sparse, lane_per_session=False):
+def gpu_pair(game, S, P, W, d, rd, mask, sparse, lane_per_session=False, fanout=False):
     b = (G.SessionBuilder(game, num_sessions=S).with_num_players(P).with_max_prediction_window(W)
          .with_input_delay(d).with_sparse_saving_mode(sparse).with_remote_input_delay(rd)
-         .with_lane_per_session(lane_per_session))
+         .with_lane_per_session(lane_per_session).with_speculative_fanout(fanout))
     for h in range(P):
         b.add_player(PlayerType.Local if (mask >> h) & 1 else PlayerType.Remote, h)
     sess = b.start_p2p_session()
@@ -204,3 +204,59 @@ def test_gpu_p2p_fused_launch_equals_per_tick(gpu_available):
     compare_state(b, orc, T - 1)
     for x, y in zip(a.read_cells(), b.read_cells()):
         np.testing.assert_array_equal(x, y)
+
+
+FANOUT_CASES = [  # P, W, d, rd, local_mask, lag range (BASELINE config 4 = P 4, W 8)
+    (4, 8, 1, 1, 0b0001, (1, 5)),
+    (2, 8, 2, 2, 0b01, (0, 6)),
+    (3, 7, 0, 0, 0b010, (1, 4)),
+    (4, 4, 0, 0, 0b0001, (1, 6)),  # PredictionThreshold hits too
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", FANOUT_CASES, ids=[f"P{c[0]}-W{c[1]}-d{c[2]}-rd{c[3]}-m{c[4]}" for c in FANOUT_CASES])
+def test_gpu_speculative_fanout_matches_rollback(gpu_available, case):
+    # With the fan-out, matching mispredictions are served by a branch select:
+    # statuses, logical request counts, cells and states must stay identical to
+    # the reference's rollback (the oracle) on every tick, and selects must
+    # actually happen.
+    import torch
+    P, W, d, rd, mask, (lo, hi) = case
+    S, T = 96, 80
+    inputs, upto, rin = synth_network(S, P, T, mask, rd, lo, hi)
+    sess, orc = gpu_pair(G.Game.EX_GAME, S, P, W, d, rd, mask, False, fanout=True)
+    di, du, dr = (torch.from_numpy(a).cuda() for a in (inputs, upto, rin))
+    for t in range(T):
+        sess.run_ticks(di[t:t + 1], du[t:t + 1], dr)
+        ost, olf, ona, ons = drive_oracle(orc, mask, inputs, upto, rin, t + 1, t0=t)[0]
+        st, lf, na, ns = sess.status()
+        np.testing.assert_array_equal(st, ost, err_msg=f"status, tick {t}")
+        np.testing.assert_array_equal(lf, olf, err_msg=f"rollback frame, tick {t}")
+        np.testing.assert_array_equal(na, ona, err_msg=f"AdvanceFrame count, tick {t}")
+        np.testing.assert_array_equal(ns, ons, err_msg=f"SaveGameState count, tick {t}")
+        if t % 8 == 7 or t == T - 1:
+            compare_state(sess, orc, t)
+    adv, saves, loads, selects, branch_frames = sess.totals()
+    assert selects > 0, "no misprediction was served by a branch select"
+    assert branch_frames > 0
+    assert sess.counters()[2] == 0
+
+
+@pytest.mark.gpu
+def test_gpu_speculative_fanout_state_after_many_ticks(gpu_available):
+    # Long run, fused call of many ticks: final cells and state equal the plain P2P batch.
+    import torch
+    P, W, d, rd, mask = 4, 8, 1, 1, 0b0001
+    S, T = 256, 160
+    inputs, upto, rin = synth_network(S, P, T, mask, rd, 1, 5)
+    di, du, dr = (torch.from_numpy(a).cuda() for a in (inputs, upto, rin))
+    spec, _ = gpu_pair(G.Game.EX_GAME, S, P, W, d, rd, mask, False, fanout=True)
+    plain, _ = gpu_pair(G.Game.EX_GAME, S, P, W, d, rd, mask, False)
+    spec.run_ticks(di, du, dr)
+    plain.run_ticks(di, du, dr)
+    np.testing.assert_array_equal(spec.read_live(), plain.read_live())
+    for x, y in zip(spec.read_cells(), plain.read_cells()):
+        np.testing.assert_array_equal(x, y)
+    ts, tp = spec.totals(), plain.totals()
+    assert ts[3] > 0 and ts[2] + ts[3] == tp[2], (ts, tp)  # every rollback is a load or a select
