@@ -106,7 +106,8 @@ def bench_p2p(args):
     di, du, dr = (torch.from_numpy(a).to(dev) for a in (inputs, upto, rin))
     b = (G.SessionBuilder(G.Game.EX_GAME, num_sessions=S, device=local).with_num_players(P)
          .with_max_prediction_window(W).with_input_delay(args.input_delay).with_remote_input_delay(args.remote_delay)
-         .with_sparse_saving_mode(args.sparse_saving).with_block_size(args.block_size))
+         .with_sparse_saving_mode(args.sparse_saving).with_block_size(args.block_size)
+         .with_speculative_fanout(args.fanout))
     for h in range(P):
         b.add_player(PlayerType.Local if (mask >> h) & 1 else PlayerType.Remote, h)
     sess = b.start_p2p_session()
@@ -137,14 +138,14 @@ def bench_p2p(args):
         elapsed = time.perf_counter() - t0
         kernel_ms, launches = sess.profile_take()
     a1 = sess.totals()
-    adv, saves, loads = (a1[i] - a0[i] for i in range(3))
+    adv, saves, loads, selects, branch = (a1[i] - a0[i] for i in range(5))
     thr, unexpected, panics = sess.counters()
-    tot = torch.tensor([adv, saves, loads, panics], dtype=torch.float64, device=dev)
+    tot = torch.tensor([adv, saves, loads, panics, selects, branch], dtype=torch.float64, device=dev)
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(tot)
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    adv, saves, loads, panics = (int(x) for x in tot.tolist())
+    adv, saves, loads, panics, selects, branch = (int(x) for x in tot.tolist())
     elapsed = float(el.item())
     if rank == 0:
         # algorithmic bytes (this rank's launches): cells loaded + saved (40 B state,
@@ -154,6 +155,9 @@ def bench_p2p(args):
         state = 4 * 5 * P
         bytes_rank = (adv / world * P + saves / world * (state + 6) + loads / world * state
                       + S * args.steps * 8)
+        if args.fanout:  # per branch frame: its cell + checksum stored; per session-tick: base cell load,
+            # 16 branch states stored, per select: the selected cells read back
+            bytes_rank += branch / world * (state + 2 + P) + S * args.steps * state * 17 + selects / world * state
         avg_kernel_s = kernel_ms / 1e3 / max(1, launches)
         achieved = bytes_rank / max(1, launches) / avg_kernel_s / 1e9
         line = {
@@ -164,16 +168,22 @@ def bench_p2p(args):
             "config": {"workload": f"ex_game P2PSession x {S} sessions/GPU, {P} players (handle 0 local), "
                                    f"max_prediction {W}, input delay {args.input_delay}, remote delay "
                                    f"{args.remote_delay}, network lag {lo}-{hi} frames"
-                                   + (", sparse saving" if args.sparse_saving else ""),
+                                   + (", sparse saving" if args.sparse_saving else "")
+                                   + (", speculative fan-out 16 candidates/frame" if args.fanout else ""),
                        "sessions_per_gpu": S, "total_sessions": S * world,
                        "advance_frames_per_session_tick": adv / (S * world * args.steps),
-                       "rollbacks_per_session_tick": loads / (S * world * args.steps),
+                       "rollbacks_per_session_tick": (loads + selects) / (S * world * args.steps),
+                       "speculative": ({"branches": 16, "selects": selects, "loads": loads,
+                                        "select_fraction": selects / max(1, selects + loads),
+                                        "branch_frames_per_s": branch / elapsed}
+                                       if args.fanout else None),
                        "prediction_threshold_hits": thr, "panics": panics,
                        "parallelism": f"session-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel_avg_us": avg_kernel_s * 1e6,
                          "ticks_per_launch": args.steps / max(1, launches), "launches_timed": launches,
-                         "kernel": f"p2p_kernel<ExGame<{P},true>> (fused P2P ticks)"},
+                         "kernel": f"p2p_kernel<ExGame<{P},true>>" + (" + fanout_kernel (per tick)" if args.fanout
+                                                                          else " (fused P2P ticks)")},
             "cpu_baseline": None,
         }
         print(json.dumps(line), flush=True)
@@ -209,6 +219,9 @@ def main():
     ap.add_argument("--lag", type=str, default="1,4", help="p2p: min,max network lag in frames")
     ap.add_argument("--remote-delay", type=int, default=2, help="p2p: the remote peers' input delay")
     ap.add_argument("--sparse-saving", action="store_true", help="p2p: with_sparse_saving_mode(true)")
+    ap.add_argument("--fanout", action="store_true",
+                    help="p2p: speculative fan-out, 16 candidate inputs per session per tick (BASELINE configs[3]; "
+                         "use with --num-players 4)")
     args = ap.parse_args()
     if args.session == "p2p":
         return bench_p2p(args)

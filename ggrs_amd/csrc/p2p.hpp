@@ -54,6 +54,9 @@ constexpr int kQsFields = QS_PLAYER0 + QF_COUNT * 4;
 // trace rows (the last tick of the last launch): LoadGameState frame, AdvanceFrame count, SaveGameState count
 enum : int { TR_LOAD = 0, TR_NADV = 1, TR_NSAVE = 2, TR_COUNT = 3 };
 constexpr int32_t kP2PStatusOk = 0, kP2PStatusThreshold = 1, kP2PStatusPanic = 101;
+// executed work: AdvanceFrames, SaveGameStates, LoadGameStates, rollbacks
+// replaced by a speculative branch select, branch frames presimulated
+enum : int { ST_ADV = 0, ST_SAVE = 1, ST_LOAD = 2, ST_SELECT = 3, ST_BRANCH = 4, ST_COUNT = 5 };
 // Speculative fan-out: branch k holds candidate input k for one remote player
 // over its unconfirmed frames (the full 4-bit ex_game alphabet).
 constexpr int kSpecBranches = 16;
@@ -71,12 +74,15 @@ struct P2PParams {
   int32_t* status;          // [Spad] rb_status of the session's last advance_frame
   int32_t* trace;           // [TR_COUNT][Spad]
   uint32_t* counters;       // [0] threshold hits, [1] unexpected-path count, [2] panics
-  unsigned long long* totals;  // executed: [0] AdvanceFrames, [1] SaveGameStates, [2] LoadGameStates,
-                               // [3] rollbacks replaced by a speculative branch select, [4] branch frames presimulated
+  // per-session work counters [ST_COUNT][Spad] (no same-address atomics: each
+  // session's lead lane owns its column; the host sums on demand)
+  unsigned long long* stats;
   // speculative fan-out (fanout_kernel below; spec_on = 0: plain P2P)
-  const uint32_t* spec_state;  // [kSpecBranches][NW planes][Spad*L] branch states at meta end
-  const uint32_t* spec_cells;  // [W][kSpecBranches][NW planes][Spad*L] branch cells
-  const void* spec_cs;         // [W][kSpecBranches][Spad] CS
+  // branch-major columns: column (s * kSpecBranches + k) * L + lane, so one
+  // session's 16 branches x L lanes store 64 consecutive words per plane
+  const uint32_t* spec_state;  // [NW planes][Spad*16*L] branch states at meta end
+  const uint32_t* spec_cells;  // [W][NW planes][Spad*16*L] branch cells
+  const void* spec_cs;         // [W][Spad][16] CS
   const int32_t* spec_meta;    // [SM_COUNT][Spad]
   int32_t spec_on;
   const uint8_t* local_in;  // tick t, handle h: local_in + t * local_stride + (h * S + s) * IB
@@ -314,20 +320,21 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     adjust(first_incorrect, min_confirmed);
     exec = true;
     if (status == kP2PStatusPanic) return true;
-    const unsigned bw = static_cast<unsigned>(NW) * Gpad;  // words of one branch block
+    const unsigned Gs = Gpad * kSpecBranches;                              // spec plane width
+    const unsigned col = (s * kSpecBranches + static_cast<unsigned>(kk)) * L + lane;  // branch kk, this lane
     const CS* __restrict__ scs = reinterpret_cast<const CS*>(p.spec_cs);
     for (int32_t f = base + 1; f < cur; ++f) {  // the cells adjust would have saved
       const unsigned slot = static_cast<unsigned>(f % W);
       uint32_t cw[NW];
-      load_words<NW>(p.spec_cells + (slot * kSpecBranches + kk) * bw, static_cast<int>(Gpad), static_cast<int>(g), cw);
+      load_words<NW>(p.spec_cells + slot * NW * Gs, static_cast<int>(Gs), static_cast<int>(col), cw);
       store_words<NW>(p.snap + slot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), cw);
       if (lead) {
-        csa[slot * Spad + s] = scs[(slot * kSpecBranches + kk) * Spad + s];
+        csa[slot * Spad + s] = scs[(slot * Spad + s) * kSpecBranches + kk];
         p.tag[slot * Spad + s] = f;
       }
       ++tot_save;
     }
-    load_words<NW>(p.spec_state + kk * bw, static_cast<int>(Gpad), static_cast<int>(g), w);
+    load_words<NW>(p.spec_state, static_cast<int>(Gs), static_cast<int>(col), w);
     ++tot_sel;
     return true;
   };
@@ -450,10 +457,10 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     p.trace[TR_NADV * Spad + s] = nadv;
     p.trace[TR_NSAVE * Spad + s] = nsave;
     if (status == kP2PStatusPanic) atomicAdd(&p.counters[2], 1u);
-    atomicAdd(&p.totals[0], static_cast<unsigned long long>(tot_adv));
-    atomicAdd(&p.totals[1], static_cast<unsigned long long>(tot_save));
-    atomicAdd(&p.totals[2], static_cast<unsigned long long>(tot_load));
-    if (tot_sel) atomicAdd(&p.totals[3], static_cast<unsigned long long>(tot_sel));
+    p.stats[ST_ADV * Spad + s] += tot_adv;
+    p.stats[ST_SAVE * Spad + s] += tot_save;
+    p.stats[ST_LOAD * Spad + s] += tot_load;
+    p.stats[ST_SELECT * Spad + s] += tot_sel;
   }
 }
 
@@ -479,7 +486,7 @@ struct FanParams {
   uint32_t* spec_cells;
   void* spec_cs;
   int32_t* spec_meta;
-  unsigned long long* totals;
+  unsigned long long* stats;  // [ST_COUNT][Spad], ST_BRANCH column
   uint32_t* counters;
   int32_t S, Spad, W;
   uint32_t local_mask;
@@ -500,7 +507,7 @@ __global__ void __launch_bounds__(256) fanout_kernel(const FanParams p) {
   const int k = r / L, lane = r % L;  // branch = candidate input, player slot
   if (s >= static_cast<unsigned>(p.S)) return;
   const unsigned Spad = static_cast<unsigned>(p.Spad), Gpad = Spad * L;
-  const unsigned bw = static_cast<unsigned>(NW) * Gpad;
+  const unsigned Gs = Gpad * kSpecBranches;  // spec plane width: column = this thread's index g
   const int W = p.W;
   const RingIO<IB> ring{const_cast<uint8_t*>(reinterpret_cast<const uint8_t*>(p.ring)), P, p.Spad};
   auto qrow = [&](int field, int h) { return p.qs[static_cast<size_t>(QS_PLAYER0 + field * 4 + h) * Spad + s]; };
@@ -530,7 +537,7 @@ __global__ void __launch_bounds__(256) fanout_kernel(const FanParams p) {
   if (!valid) return;  // session-uniform: the whole group leaves
   const unsigned gl = s * L + lane;  // this lane's column in the session-major planes
   uint32_t w[NW];
-  load_words<NW>(p.snap + static_cast<unsigned>(base % W) * bw, static_cast<int>(Gpad), static_cast<int>(gl), w);
+  load_words<NW>(p.snap + static_cast<unsigned>(base % W) * NW * Gpad, static_cast<int>(Gpad), static_cast<int>(gl), w);
   // this lane's player: its inputs over the window, as adjust_gamestate would see them
   const int h = lane;
   const bool active = h < P;
@@ -544,8 +551,8 @@ __global__ void __launch_bounds__(256) fanout_kernel(const FanParams p) {
       CsCtx ctx{0ull, s, 0u};
       const CS c = G::checksum(w, f, lane, ctx);
       const unsigned slot = static_cast<unsigned>(f % W);
-      store_words<NW>(p.spec_cells + (slot * kSpecBranches + k) * bw, static_cast<int>(Gpad), static_cast<int>(gl), w);
-      if (lane == 0) cs[(slot * kSpecBranches + k) * Spad + s] = c;
+      store_words<NW>(p.spec_cells + slot * NW * Gs, static_cast<int>(Gs), static_cast<int>(g), w);
+      if (lane == 0) cs[(slot * Spad + s) * kSpecBranches + k] = c;
     }
     uint32_t v = 0;
     if (active) {
@@ -557,8 +564,8 @@ __global__ void __launch_bounds__(256) fanout_kernel(const FanParams p) {
                &p.counters[1]);
     ++frames;
   }
-  store_words<NW>(p.spec_state + k * bw, static_cast<int>(Gpad), static_cast<int>(gl), w);
-  if (lane == 0) atomicAdd(&p.totals[4], static_cast<unsigned long long>(frames));
+  store_words<NW>(p.spec_state, static_cast<int>(Gs), static_cast<int>(g), w);
+  if (k == 0 && lane == 0) p.stats[ST_BRANCH * Spad + s] += static_cast<unsigned long long>(frames) * kSpecBranches;
 }
 
 }  // namespace rb

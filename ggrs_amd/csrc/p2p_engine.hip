@@ -24,7 +24,7 @@ struct rb_p2p {
   int32_t* status = nullptr;
   int32_t* trace = nullptr;
   uint32_t* counters = nullptr;
-  unsigned long long* totals = nullptr;
+  unsigned long long* stats = nullptr;  // [ST_COUNT][Spad]
   bool fanout = false;
   uint32_t* spec_state = nullptr;
   uint32_t* spec_cells = nullptr;
@@ -54,7 +54,7 @@ void free_all(rb_p2p* b) {
   (void)hipSetDevice(b->device);
   if (b->stream) (void)hipStreamSynchronize(b->stream);
   void* ptrs[] = {b->snap,   b->cs,      b->tag,       b->ring,       b->live,    b->qs,       b->status,
-                  b->trace,  b->counters, b->totals, b->spec_state, b->spec_cells, b->spec_cs, b->spec_meta};
+                  b->trace,  b->counters, b->stats, b->spec_state, b->spec_cells, b->spec_cs, b->spec_meta};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   for (auto& pr : b->prof_ev) {
@@ -163,7 +163,7 @@ rb_status rb_p2p_create(const rb_p2p_config* cfg, rb_p2p** out) {
   P2P_CREATE(hipMalloc(&b->status, Sp * 4));
   P2P_CREATE(hipMalloc(&b->trace, TR_COUNT * Sp * 4));
   P2P_CREATE(hipMalloc(&b->counters, 16));
-  P2P_CREATE(hipMalloc(&b->totals, 64));
+  P2P_CREATE(hipMalloc(&b->stats, ST_COUNT * Sp * 8));
   P2P_CREATE(hipMemsetAsync(b->snap, 0, W * NW * Gp * 4, b->stream));
   P2P_CREATE(hipMemsetAsync(b->cs, 0, W * Sp * b->ops->cs_bytes, b->stream));
   P2P_CREATE(hipMemsetAsync(b->tag, 0xff, W * Sp * 4, b->stream));  // GameState::default frame = NULL_FRAME
@@ -171,7 +171,7 @@ rb_status rb_p2p_create(const rb_p2p_config* cfg, rb_p2p** out) {
   P2P_CREATE(hipMemsetAsync(b->status, 0, Sp * 4, b->stream));
   P2P_CREATE(hipMemsetAsync(b->trace, 0xff, TR_COUNT * Sp * 4, b->stream));
   P2P_CREATE(hipMemsetAsync(b->counters, 0, 16, b->stream));
-  P2P_CREATE(hipMemsetAsync(b->totals, 0, 64, b->stream));
+  P2P_CREATE(hipMemsetAsync(b->stats, 0, ST_COUNT * Sp * 8, b->stream));
   if (b->fanout) {
     const size_t K = kSpecBranches;
     P2P_CREATE(hipMalloc(&b->spec_state, K * NW * Gp * 4));
@@ -231,7 +231,7 @@ rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs,
   p.status = b->status;
   p.trace = b->trace;
   p.counters = b->counters;
-  p.totals = b->totals;
+  p.stats = b->stats;
   p.local_in = static_cast<const uint8_t*>(local_inputs);
   p.local_stride = local_stride;
   p.upto = remote_upto;
@@ -260,7 +260,7 @@ rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs,
   fp.spec_cells = b->spec_cells;
   fp.spec_cs = b->spec_cs;
   fp.spec_meta = b->spec_meta;
-  fp.totals = b->totals;
+  fp.stats = b->stats;
   fp.counters = b->counters;
   fp.S = b->S;
   fp.Spad = b->Spad;
@@ -373,10 +373,14 @@ rb_status rb_p2p_counters(rb_p2p* b, uint32_t* out3) {
 }
 
 rb_status rb_p2p_totals(rb_p2p* b, uint64_t* out5) {
-  unsigned long long c[8];
-  P2P_TRY(b, hipStreamSynchronize(b->stream));
-  P2P_TRY(b, hipMemcpy(c, b->totals, 64, hipMemcpyDeviceToHost));
-  for (int i = 0; i < 5; ++i) out5[i] = c[i];
+  std::vector<unsigned long long> st;
+  rb_status r = read_rows(b, b->stats, ST_COUNT, st);
+  if (r != RB_OK) return r;
+  for (int i = 0; i < ST_COUNT; ++i) {
+    uint64_t t = 0;
+    for (int s = 0; s < b->S; ++s) t += st[static_cast<size_t>(i) * b->Spad + s];
+    out5[i] = t;
+  }
   return RB_OK;
 }
 
