@@ -127,6 +127,10 @@ SIGNATURES = [
     ("rb_p2p_totals", _I32, [_P, _P]),
     ("rb_p2p_profile_enable", _I32, [_P, _I32]),
     ("rb_p2p_profile_take", _I32, [_P, ctypes.POINTER(ctypes.c_double), _PI32]),
+    ("rb_decode_input_packets", _I32, [_I32, _P, _I32, _I32, _I32, _I32, _I32, _P, ctypes.c_int64, _P, _P, _P, _I32,
+                                        _P, _P]),
+    ("rb_encode_input_packets", _I32, [_I32, _P, _I32, _I32, _I32, _I32, _P, _I32, _I32, _P, _P, _P, ctypes.c_int64,
+                                        _P, _P]),
 ]
 
 _lib = None

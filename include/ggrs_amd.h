@@ -285,6 +285,42 @@ rb_status rb_p2p_totals(rb_p2p* b, uint64_t* out5);
 rb_status rb_p2p_profile_enable(rb_p2p* b, int32_t on);
 rb_status rb_p2p_profile_take(rb_p2p* b, double* total_ms, int32_t* launches);
 
+/* ===========================================================================
+ * Batched input packets (network/compression.rs): one
+ * endpoint per (session, remote handle), one packet per endpoint per call.
+ * Wire format: XOR delta of every pending input against the reference input,
+ * then bitfield RLE (bitfield-rle 0.2 format).  All pointers are device
+ * memory; `stream` is a hipStream_t (NULL: the null stream).
+ * ======================================================================== */
+
+/* UdpProtocol::on_input (protocol.rs:616-689) for every session's endpoint of
+ * remote handle `handle`: packet s is packets + s*packet_stride, lengths[s]
+ * bytes (0: none), covering frames start_frames[s]... .  It is decoded against
+ * the input before its start frame (remote_inputs, or the zeroed input before
+ * the first one), inputs of frames after remote_upto[handle][s] are written to
+ * remote_inputs[frame][num_players][num_sessions] (input_bytes each) and
+ * remote_upto advances: exactly the delivery tensors rb_p2p_run_ticks reads.
+ * status[s]: 0 new inputs, 1 nothing new, -1 malformed (the reference panics:
+ * "decoding failed"), -2 frames missing before start_frame (reference assert).
+ * A packet whose reference input is older than 2*max_prediction frames is
+ * ignored (recv_inputs retention, protocol.rs:686-688). */
+rb_status rb_decode_input_packets(int32_t device, void* stream, int32_t handle, int32_t num_players,
+                                  int32_t num_sessions, int32_t input_bytes, int32_t max_prediction,
+                                  const uint8_t* packets, int64_t packet_stride, const int32_t* lengths,
+                                  const int32_t* start_frames, void* remote_inputs, int32_t remote_frames,
+                                  int32_t* remote_upto, int32_t* status);
+
+/* UdpProtocol::send_pending_output (protocol.rs:468-500) for every session's
+ * endpoint: the inputs of handle `handle` for frames acked[s]+1 .. newest[s]
+ * (first_frame .. newest[s] before any ack: the sender's input delay) from
+ * inputs[frame][num_players][num_sessions], encoded against the input of frame
+ * acked[s] (zeroed when acked[s] = RB_NULL_FRAME).  Writes the packet, its
+ * length (0: nothing pending, -1: larger than packet_stride) and start frame. */
+rb_status rb_encode_input_packets(int32_t device, void* stream, int32_t handle, int32_t num_players,
+                                  int32_t num_sessions, int32_t input_bytes, const void* inputs, int32_t frames,
+                                  int32_t first_frame, const int32_t* acked, const int32_t* newest, uint8_t* packets,
+                                  int64_t packet_stride, int32_t* lengths, int32_t* start_frames);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

@@ -1099,4 +1099,104 @@ struct SynthInput {
   }
 };
 
+// ===========================================================================
+// network/compression.rs (XOR delta + bitfield RLE) — the input wire format
+// that UdpProtocol::on_input decodes (protocol.rs:616-689).
+// bitfield-rle 0.2 (Cargo.toml:23) is not vendored: its published format is
+// restated (a series of varint-headed sequences; odd header = compressed run
+// `len << 2 | bit << 1 | 1` of 0x00 / 0xFF bytes, even header = `len << 1`
+// followed by len literal bytes; varints are unsigned LEB128).  Decoding is
+// defined by that format.  The encoder's choice of which runs to compress is
+// the crate's own heuristic, not pinned by any reference test (the only one,
+// compression.rs:81-90, is a round trip): here runs of >= 4 equal 0x00/0xFF
+// bytes are compressed — parity unpinned for encoded bytes, pinned for decode
+// and for round trips.
+// ===========================================================================
+namespace wire {
+inline void varint_put(std::vector<uint8_t>& out, uint64_t v) {
+  while (v >= 0x80) {
+    out.push_back(static_cast<uint8_t>(v | 0x80));
+    v >>= 7;
+  }
+  out.push_back(static_cast<uint8_t>(v));
+}
+// returns false on a truncated or over-long varint
+inline bool varint_get(const uint8_t* d, size_t n, size_t& p, uint64_t& v) {
+  v = 0;
+  for (int shift = 0; shift < 64; shift += 7) {
+    if (p >= n) return false;
+    const uint8_t b = d[p++];
+    v |= static_cast<uint64_t>(b & 0x7F) << shift;
+    if (!(b & 0x80)) return true;
+  }
+  return false;
+}
+constexpr size_t kRunMin = 4;
+inline std::vector<uint8_t> rle_encode(const std::vector<uint8_t>& bits) {  // bitfield_rle::encode
+  std::vector<uint8_t> out;
+  size_t i = 0, lit = 0;  // literal segment [lit, i)
+  auto flush = [&](size_t end) {
+    if (end > lit) {
+      varint_put(out, static_cast<uint64_t>(end - lit) << 1);
+      out.insert(out.end(), bits.begin() + static_cast<long>(lit), bits.begin() + static_cast<long>(end));
+    }
+  };
+  while (i < bits.size()) {
+    const uint8_t b = bits[i];
+    size_t j = i;
+    if (b == 0x00 || b == 0xFF)
+      while (j < bits.size() && bits[j] == b) ++j;
+    if (j - i >= kRunMin) {
+      flush(i);
+      varint_put(out, (static_cast<uint64_t>(j - i) << 2) | (b ? 2u : 0u) | 1u);
+      i = lit = j;
+    } else {
+      i = j > i ? j : i + 1;
+    }
+  }
+  flush(bits.size());
+  return out;
+}
+// bitfield_rle::decode: false on malformed input (the reference's
+// `.expect("decoding failed")` panics, protocol.rs:656)
+inline bool rle_decode(const uint8_t* d, size_t n, std::vector<uint8_t>& out) {
+  out.clear();
+  size_t p = 0;
+  while (p < n) {
+    uint64_t h;
+    if (!varint_get(d, n, p, h)) return false;
+    if (h & 1) {
+      const uint64_t len = h >> 2;
+      if (len > (1u << 16)) return false;
+      out.insert(out.end(), static_cast<size_t>(len), (h & 2) ? 0xFF : 0x00);
+    } else {
+      const uint64_t len = h >> 1;
+      if (len > n - p) return false;
+      out.insert(out.end(), d + p, d + p + len);
+      p += static_cast<size_t>(len);
+    }
+  }
+  return true;
+}
+// compression.rs:3-11 encode = delta_encode (:13-30) then RLE
+inline std::vector<uint8_t> encode(const std::vector<uint8_t>& ref, const std::vector<std::vector<uint8_t>>& pending) {
+  std::vector<uint8_t> bytes;
+  for (auto& in : pending) {
+    ORC_ASSERT(in.size() == ref.size());
+    for (size_t i = 0; i < ref.size(); ++i) bytes.push_back(ref[i] ^ in[i]);
+  }
+  return rle_encode(bytes);
+}
+// compression.rs:32-57 decode = RLE decode then delta_decode
+inline bool decode(const std::vector<uint8_t>& ref, const uint8_t* d, size_t n, std::vector<std::vector<uint8_t>>& out) {
+  std::vector<uint8_t> buf;
+  if (!rle_decode(d, n, buf)) return false;
+  ORC_ASSERT(!ref.empty() && buf.size() % ref.size() == 0);
+  out.assign(buf.size() / ref.size(), std::vector<uint8_t>(ref.size()));
+  for (size_t k = 0; k < out.size(); ++k)
+    for (size_t i = 0; i < ref.size(); ++i) out[k][i] = ref[i] ^ buf[ref.size() * k + i];
+  return true;
+}
+}  // namespace wire
+
 }  // namespace orc

@@ -61,6 +61,8 @@ def load():
             "orc_p2p_read_cells": (I32, [P, P, P, P]),
             "orc_p2p_read_live": (I32, [P, P, P]),
             "orc_p2p_frames": (I32, [P, P, P]),
+            "orc_wire_encode": (I32, [P, I32, P, I32, P, I32]),
+            "orc_wire_decode": (I32, [P, I32, P, I32, P, I32]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
@@ -261,3 +263,25 @@ def bench_brawler(num_players: int, check_distance: int, input_delay: int, max_p
     t = load().orc_bench_brawler(num_players, check_distance, input_delay, max_prediction, sessions, warmup, ticks,
                                  threads, seed, ctypes.byref(ne))
     return t, ne.value
+
+
+def wire_encode(ref: bytes, inputs) -> bytes:
+    """compression.rs encode: XOR delta of every input against ref, then bitfield RLE (TEST ONLY)."""
+    r = np.frombuffer(bytes(ref), np.uint8)
+    a = np.ascontiguousarray(np.asarray(inputs, np.uint8).reshape(-1, r.size))
+    out = np.zeros(16 + 2 * a.size + 8, np.uint8)
+    n = load().orc_wire_encode(_ptr(r), r.size, _ptr(a) if a.size else None, a.shape[0], _ptr(out), out.size)
+    assert n >= 0
+    return out[:n].tobytes()
+
+
+def wire_decode(ref: bytes, data: bytes, cap: int = 4096):
+    """compression.rs decode; None when malformed (the reference panics) (TEST ONLY)."""
+    r = np.frombuffer(bytes(ref), np.uint8)
+    d = np.frombuffer(bytes(data) or b"\0", np.uint8)
+    out = np.zeros((cap, r.size), np.uint8)
+    n = load().orc_wire_decode(_ptr(r), r.size, _ptr(d), len(data), _ptr(out), cap)
+    if n == -1:
+        return None
+    assert n >= 0
+    return out[:n]

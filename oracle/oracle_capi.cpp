@@ -455,6 +455,34 @@ int32_t orc_p2p_frames(void* b, int32_t* current, int32_t* confirmed) {
   return static_cast<P2PBatchBase*>(b)->frames(current, confirmed);
 }
 
+// network/compression.rs wire format (ggrs_oracle.hpp namespace wire).
+// encode: n inputs of ref_len bytes against ref; returns the encoded length or
+// -1 if cap is too small.  decode: returns the number of inputs, -1 malformed,
+// -2 if cap is too small.
+int32_t orc_wire_encode(const uint8_t* ref, int32_t ref_len, const uint8_t* inputs, int32_t n, uint8_t* out,
+                        int32_t cap) {
+  std::vector<uint8_t> r(ref, ref + ref_len);
+  std::vector<std::vector<uint8_t>> pend;
+  for (int32_t k = 0; k < n; ++k) pend.emplace_back(inputs + k * ref_len, inputs + (k + 1) * ref_len);
+  auto e = wire::encode(r, pend);
+  if (static_cast<int32_t>(e.size()) > cap) return -1;
+  std::memcpy(out, e.data(), e.size());
+  return static_cast<int32_t>(e.size());
+}
+int32_t orc_wire_decode(const uint8_t* ref, int32_t ref_len, const uint8_t* data, int32_t len, uint8_t* out,
+                        int32_t cap_inputs) {
+  std::vector<uint8_t> r(ref, ref + ref_len);
+  std::vector<std::vector<uint8_t>> dec;
+  try {
+    if (!wire::decode(r, data, static_cast<size_t>(len), dec)) return -1;
+  } catch (const Panic&) {
+    return -1;
+  }
+  if (static_cast<int32_t>(dec.size()) > cap_inputs) return -2;
+  for (size_t k = 0; k < dec.size(); ++k) std::memcpy(out + k * ref_len, dec[k].data(), ref_len);
+  return static_cast<int32_t>(dec.size());
+}
+
 // Third-party arithmetic, exposed for the known-answer tests.
 uint16_t orc_fletcher16(const uint8_t* d, uint64_t n) { return fletcher16(d, n); }
 uint64_t orc_siphash(int32_t c, int32_t d, uint64_t k0, uint64_t k1, const uint8_t* m, uint64_t n) {

@@ -8,6 +8,7 @@
 //   src/sync_layer.rs:301-343           (2 tests)
 //   tests/test_synctest_session.rs      (5 tests)
 //   tests/test_synctest_session_enum.rs (1 test)
+//   src/network/compression.rs:81-90    (1 test)
 // plus the published vectors for the third-party arithmetic on the path
 // (fletcher16, SipHash).  Run by tests/test_oracle.py; exits non-zero on any
 // failure and prints one line per test.
@@ -43,6 +44,15 @@ static void run(const char* name, const std::function<void()>& fn, bool should_p
 struct TestInput { uint8_t inp; };  // input_queue.rs:255-259, sync_layer.rs:287-291
 
 int main() {
+  // ---- network/compression.rs:81-90 -------------------------------------------
+  run("compression::test_encode_decode", [] {
+    std::vector<uint8_t> ref{0, 0, 0, 1};
+    std::vector<std::vector<uint8_t>> pend{{0, 0, 1, 0}, {0, 0, 1, 1}, {0, 1, 0, 0}, {0, 1, 0, 1}, {0, 1, 1, 0}};
+    auto enc = wire::encode(ref, pend);
+    std::vector<std::vector<uint8_t>> dec;
+    CHECK(wire::decode(ref, enc.data(), enc.size(), dec));
+    CHECK(dec == pend);
+  });
   // ---- frame_info.rs:83-102 ------------------------------------------------
   run("frame_info::test_input_equality", [] {
     PlayerInput<TestInput> a(0, {5}), b(0, {5});

@@ -1,0 +1,211 @@
+"""Batched input packets: network/compression.rs's wire
+format (XOR delta + bitfield RLE) restated in the oracle and on the device.
+
+Pinning: the reference's only test of the format is the round trip of
+compression.rs:81-90 (restated in oracle/ref_tests.cpp and here).  bitfield-rle
+0.2 is not vendored: decoding follows its published format, which defines the
+decoded bytes; the encoder's choice of runs to compress is this build's
+(runs >= 4 bytes), so encoded bytes are "parity unpinned" against the crate
+(device == oracle byte for byte is still checked).
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+
+def rand_inputs(rng, n, ib):
+    # hold-model streams: long repeats XOR to zero runs, as on the wire
+    vals = rng.integers(0, 256, (n, ib), dtype=np.uint8)
+    keep = rng.random(n) < 0.7
+    for i in range(1, n):
+        if keep[i]:
+            vals[i] = vals[i - 1]
+    return vals
+
+
+def test_reference_round_trip_vector():
+    # compression.rs:81-90
+    ref = bytes([0, 0, 0, 1])
+    pend = [[0, 0, 1, 0], [0, 0, 1, 1], [0, 1, 0, 0], [0, 1, 0, 1], [0, 1, 1, 0]]
+    enc = O.wire_encode(ref, pend)
+    assert O.wire_decode(ref, enc).tolist() == pend
+
+
+@pytest.mark.parametrize("ib", [1, 2, 4])
+def test_random_round_trips_and_compression(ib):
+    rng = np.random.default_rng(ib)
+    saw_run = False
+    for _ in range(300):
+        n = int(rng.integers(1, 40))
+        ref = rng.integers(0, 256, ib, dtype=np.uint8).tobytes()
+        ins = rand_inputs(rng, n, ib)
+        if rng.random() < 0.3:
+            ins[:] = np.frombuffer(ref, np.uint8)  # all equal to the reference: one zero run
+        enc = O.wire_encode(ref, ins)
+        dec = O.wire_decode(ref, enc)
+        np.testing.assert_array_equal(dec, ins)
+        saw_run |= any(b & 1 for b in enc[:1])
+    assert saw_run
+
+
+def test_malformed_packets_are_rejected():
+    ref = b"\x00"
+    assert O.wire_decode(ref, bytes([0x80])) is None          # truncated varint
+    assert O.wire_decode(ref, bytes([0x06, 0x01])) is None    # literal of 3 bytes, 1 present
+    assert O.wire_decode(ref, bytes([0x02, 0x07])).tolist() == [[7]]
+
+
+# ---------------------------------------------------------------------------- device
+def on_input_reference(last, start, data, ref_input, max_pred, ib):
+    """protocol.rs:616-689 for one endpoint: (new inputs by frame, new last, status)."""
+    if len(data) == 0:
+        return {}, last, 1
+    if last != -1 and last + 1 < start:
+        return {}, last, -2
+    if last != -1 and start - 1 < last - 2 * max_pred:
+        return {}, last, 1
+    ref = bytes(ib) if (last == -1 or start - 1 == -1) else ref_input
+    dec = O.wire_decode(ref, data)
+    if dec is None:
+        return {}, last, -1
+    out = {}
+    for i, inp in enumerate(dec):
+        f = start + i
+        if f > last:
+            out[f] = inp.tobytes()
+    new_last = max(out) if out else last
+    return out, new_last, 0 if out else 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ib", [1, 4])
+def test_gpu_encode_matches_oracle_and_decode_matches_on_input(gpu_available, ib):
+    import ctypes
+
+    import torch
+
+    from ggrs_amd import _lib as L
+    lib = L.load()
+    rng = np.random.default_rng(100 + ib)
+    S, P, h, F, W, stride = 3000, 2, 1, 64, 8, 96
+    dt = np.uint8 if ib == 1 else np.uint32
+    inputs = np.zeros((F, P, S), dt)
+    for s in range(S):
+        inputs[:, h, s] = rand_inputs(rng, F, ib).view(dt).reshape(F)
+    acked = rng.integers(-1, 30, S).astype(np.int32)
+    newest = (acked + rng.integers(0, 12, S)).astype(np.int32)
+    d_in = torch.from_numpy(inputs).cuda()
+    d_ack, d_new = torch.from_numpy(acked).cuda(), torch.from_numpy(newest).cuda()
+    pk = torch.zeros((S, stride), dtype=torch.uint8, device="cuda")
+    ln = torch.zeros(S, dtype=torch.int32, device="cuda")
+    st = torch.zeros(S, dtype=torch.int32, device="cuda")
+    p = lambda t: ctypes.c_void_p(t.data_ptr())
+    assert lib.rb_encode_input_packets(0, None, h, P, S, ib, p(d_in), F, 0, p(d_ack), p(d_new), p(pk), stride, p(ln),
+                                       p(st)) == 0
+    torch.cuda.synchronize()
+    pk_h, ln_h, st_h = pk.cpu().numpy(), ln.cpu().numpy(), st.cpu().numpy()
+    raw = inputs.view(np.uint8).reshape(F, P, S, ib)
+    for s in range(S):
+        assert st_h[s] == acked[s] + 1
+        n = newest[s] - acked[s]
+        if n <= 0:
+            assert ln_h[s] == 0
+            continue
+        ref = bytes(ib) if acked[s] == -1 else raw[acked[s], h, s].tobytes()
+        want = O.wire_encode(ref, raw[acked[s] + 1:newest[s] + 1, h, s])
+        assert pk_h[s, :ln_h[s]].tobytes() == want, s
+    # decode: receiver state `last` per session, some packets corrupted / gapped / stale
+    last = rng.integers(-1, 40, S).astype(np.int32)
+    recv = np.zeros((F, P, S), dt)
+    recv[:, h, :] = inputs[:, h, :]  # frames <= last are known to the receiver
+    start = st_h.copy()
+    lens = ln_h.copy()
+    bad = rng.random(S) < 0.05
+    pk_h2 = pk_h.copy()
+    for s in np.nonzero(bad)[0]:
+        if lens[s] > 0:
+            lens[s] = max(1, lens[s] - 1)
+            pk_h2[s, lens[s] - 1] |= 0x80  # truncated varint / literal
+    upto = np.full((P, S), -1, np.int32)
+    upto[h] = last
+    d_recv = torch.from_numpy(recv).cuda()
+    d_upto = torch.from_numpy(upto).cuda()
+    d_pk = torch.from_numpy(pk_h2).cuda()
+    d_len, d_start = torch.from_numpy(lens).cuda(), torch.from_numpy(start).cuda()
+    d_st = torch.zeros(S, dtype=torch.int32, device="cuda")
+    assert lib.rb_decode_input_packets(0, None, h, P, S, ib, W, p(d_pk), stride, p(d_len), p(d_start), p(d_recv), F,
+                                       p(d_upto), p(d_st)) == 0
+    torch.cuda.synchronize()
+    got_recv = d_recv.cpu().numpy().view(np.uint8).reshape(F, P, S, ib)
+    got_upto, got_st = d_upto.cpu().numpy(), d_st.cpu().numpy()
+    kinds = set()
+    for s in range(S):
+        refin = raw[start[s] - 1, h, s].tobytes() if start[s] >= 1 else bytes(ib)
+        out, nl, code = on_input_reference(int(last[s]), int(start[s]), pk_h2[s, :lens[s]].tobytes(), refin, W, ib)
+        kinds.add(code)
+        assert got_st[s] == code, (s, got_st[s], code)
+        assert got_upto[h, s] == nl
+        for f, b in out.items():
+            assert got_recv[f, h, s].tobytes() == b
+    assert {0, 1, -1, -2} <= kinds
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P,mask,rd", [(2, 0b01, 2), (4, 0b0001, 1)])
+def test_gpu_p2p_fed_through_the_wire_equals_direct_delivery(gpu_available, P, mask, rd):
+    # Remote peers encode their pending inputs on the device (re-sending up to 2
+    # already-received frames, as an un-acked sender does), the receiver decodes
+    # them on the device into the delivery tensors, and the P2P batch runs on
+    # them: cells and state must equal a batch fed the same deliveries directly.
+    import ctypes
+
+    import torch
+
+    import ggrs_amd as G
+    from ggrs_amd import _lib as L
+    from ggrs_amd.p2p import PlayerType, synth_network
+    lib = L.load()
+    S, W, T, stride = 512, 8, 96, 64
+    inputs, upto, rin = synth_network(S, P, T, mask, rd, 1, 5)
+    F = rin.shape[0]
+
+    def batch():
+        b = (G.SessionBuilder(G.Game.EX_GAME, num_sessions=S).with_num_players(P).with_max_prediction_window(W)
+             .with_input_delay(1).with_remote_input_delay(rd))
+        for hh in range(P):
+            b.add_player(PlayerType.Local if (mask >> hh) & 1 else PlayerType.Remote, hh)
+        return b.start_p2p_session()
+
+    direct, wired = batch(), batch()
+    di, du, dr = (torch.from_numpy(a).cuda() for a in (inputs, upto, rin))
+    recv = torch.zeros_like(dr)
+    rupto = torch.full((P, S), -1, dtype=torch.int32, device="cuda")
+    pk = torch.zeros((S, stride), dtype=torch.uint8, device="cuda")
+    ln = torch.zeros(S, dtype=torch.int32, device="cuda")
+    st = torch.zeros(S, dtype=torch.int32, device="cuda")
+    dst = torch.zeros(S, dtype=torch.int32, device="cuda")
+    rng = np.random.default_rng(3)
+    p = lambda t: ctypes.c_void_p(t.data_ptr())
+    for t in range(T):
+        direct.run_ticks(di[t:t + 1], du[t:t + 1], dr)
+        for hh in range(P):
+            if (mask >> hh) & 1:
+                continue
+            redo = torch.from_numpy(rng.integers(0, 3, S).astype(np.int32)).cuda()
+            acked = torch.where(rupto[hh] < 0, rupto[hh], torch.clamp(rupto[hh] - redo, min=rd - 1))
+            acked = torch.where(acked < rd, torch.full_like(acked, -1), acked).contiguous()
+            newest = du[t, hh].contiguous()
+            assert lib.rb_encode_input_packets(0, None, hh, P, S, 1, p(dr), F, rd, p(acked), p(newest), p(pk), stride,
+                                               p(ln), p(st)) == 0
+            assert lib.rb_decode_input_packets(0, None, hh, P, S, 1, W, p(pk), stride, p(ln), p(st), p(recv), F,
+                                               p(rupto), p(dst)) == 0
+            assert int((dst < 0).sum()) == 0
+        torch.cuda.synchronize()
+        wired.run_ticks(di[t:t + 1], rupto[None].clone(), recv)
+    np.testing.assert_array_equal(rupto.cpu().numpy()[[hh for hh in range(P) if not (mask >> hh) & 1]],
+                                  upto[-1][[hh for hh in range(P) if not (mask >> hh) & 1]])
+    np.testing.assert_array_equal(wired.read_live(), direct.read_live())
+    for x, y in zip(wired.read_cells(), direct.read_cells()):
+        np.testing.assert_array_equal(x, y)
+    assert wired.totals()[2] > 0  # rollbacks happened on the wire-fed batch too
