@@ -114,11 +114,33 @@ def bench_p2p(args):
     stream = torch.cuda.Stream(device=dev)
     sess.set_stream(stream)
     tpl = args.ticks_per_launch
+    if args.wire:  # receiver-side delivery tensors, filled only by packet decode
+        import ctypes
+        lib = G._lib.load()
+        F = dr.shape[0]
+        stride = 64
+        recv = torch.zeros_like(dr)
+        rupto = torch.full((P, S), -1, dtype=torch.int32, device=dev)
+        pk = torch.zeros((S, stride), dtype=torch.uint8, device=dev)
+        ln, st, dst = (torch.zeros(S, dtype=torch.int32, device=dev) for _ in range(3))
+        ptr = lambda t: ctypes.c_void_p(t.data_ptr())
+        sp = ctypes.c_void_p(stream.cuda_stream)
+        remotes = [h for h in range(P) if not (mask >> h) & 1]
 
     def run(t0, t1):
-        for t in range(t0, t1, tpl):
-            e = min(t1, t + tpl)
-            sess.run_ticks(di[t:e], du[t:e], dr)
+        if not args.wire:
+            for t in range(t0, t1, tpl):
+                e = min(t1, t + tpl)
+                sess.run_ticks(di[t:e], du[t:e], dr)
+            return
+        for t in range(t0, t1):
+            for h in remotes:  # each remote peer sends what it has since our last receipt; we decode it
+                acked = rupto[h]  # the peer's last acked frame = our newest received (NULL before any)
+                assert lib.rb_encode_input_packets(local, sp, h, P, S, 1, ptr(dr), F, args.remote_delay, ptr(acked),
+                                                   ptr(du[t, h]), ptr(pk), stride, ptr(ln), ptr(st)) == 0
+                assert lib.rb_decode_input_packets(local, sp, h, P, S, 1, W, ptr(pk), stride, ptr(ln), ptr(st),
+                                                   ptr(recv), F, ptr(rupto), ptr(dst)) == 0
+            sess.run_ticks(di[t:t + 1], rupto[None], recv)
 
     with torch.cuda.stream(stream):
         run(0, args.warmup)
@@ -169,7 +191,9 @@ def bench_p2p(args):
                                    f"max_prediction {W}, input delay {args.input_delay}, remote delay "
                                    f"{args.remote_delay}, network lag {lo}-{hi} frames"
                                    + (", sparse saving" if args.sparse_saving else "")
-                                   + (", speculative fan-out 16 candidates/frame" if args.fanout else ""),
+                                   + (", speculative fan-out 16 candidates/frame" if args.fanout else "")
+                                   + (", inputs delivered as packets (device encode + decode per tick)"
+                                      if args.wire else ""),
                        "sessions_per_gpu": S, "total_sessions": S * world,
                        "advance_frames_per_session_tick": adv / (S * world * args.steps),
                        "rollbacks_per_session_tick": (loads + selects) / (S * world * args.steps),
@@ -219,6 +243,9 @@ def main():
     ap.add_argument("--lag", type=str, default="1,4", help="p2p: min,max network lag in frames")
     ap.add_argument("--remote-delay", type=int, default=2, help="p2p: the remote peers' input delay")
     ap.add_argument("--sparse-saving", action="store_true", help="p2p: with_sparse_saving_mode(true)")
+    ap.add_argument("--wire", action="store_true",
+                    help="p2p: remote inputs travel as packets each tick: device encode (send_pending_output) + "
+                         "decode (on_input) into the delivery tensors, then one P2P tick")
     ap.add_argument("--fanout", action="store_true",
                     help="p2p: speculative fan-out, 16 candidate inputs per session per tick (BASELINE configs[3]; "
                          "use with --num-players 4)")
