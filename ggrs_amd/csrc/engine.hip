@@ -644,10 +644,19 @@ rb_status rb_read_cell(rb_batch* b, int32_t frame, void* images, uint64_t* check
   std::vector<uint8_t> csh(static_cast<size_t>(b->Spad) * b->ops->cs_bytes);
   HIP_TRY(b, hipMemcpy(csh.data(), static_cast<uint8_t*>(b->cs) + slot * b->Spad * b->ops->cs_bytes, csh.size(),
                        hipMemcpyDeviceToHost));
+  // A session that stopped on MismatchedChecksum keeps the cells of its last
+  // tick: its slot holds the newest frame <= (its final frame - 1) of that slot.
+  std::vector<int32_t> stop(static_cast<size_t>(b->Spad));
+  HIP_TRY(b, hipMemcpy(stop.data(), b->live_frame, stop.size() * 4, hipMemcpyDeviceToHost));
   std::vector<uint32_t> w(b->ops->nw * b->ops->lanes);
   for (int s = 0; s < b->S; ++s) {
     words_of(b, planes, s, w.data());
-    if (images) b->ops->image(w.data(), frame, static_cast<uint8_t*>(images) + static_cast<size_t>(s) * b->ops->image_bytes);
+    int32_t f = frame;
+    if (stop[s] != kNullFrame) {
+      const int32_t last = stop[s] - 1;
+      f = last - ((last - static_cast<int32_t>(slot)) % b->W + b->W) % b->W;
+    }
+    if (images) b->ops->image(w.data(), f, static_cast<uint8_t*>(images) + static_cast<size_t>(s) * b->ops->image_bytes);
     if (checksums) {
       U128 c = b->ops->cs_at(csh.data(), s);
       checksums[2 * s] = c.lo;

@@ -168,13 +168,16 @@ struct ExGame {
     float vx = old_vx * kFriction;
     float vy = old_vy * kFriction;
     const bool up = input & 1u, down = input & 2u, left = input & 4u, right = input & 8u;
-    if (up != down) {  // thrust (:281-284) or brake (:286-289): exactly one of them
+    {  // thrust (:281-284) / brake (:286-289) and rotation (:291-296) as selects: some lane of
+       // every wave needs each of them, so branches only add exec-mask bookkeeping
       const SinCos sc = sincosf_glibc(rot, unexpected);
       const float tx = kMovementSpeed * sc.c, ty = kMovementSpeed * sc.s;
-      vx = up ? vx + tx : vx - tx;
-      vy = up ? vy + ty : vy - ty;
+      const float vx1 = up ? vx + tx : vx - tx, vy1 = up ? vy + ty : vy - ty;
+      vx = up != down ? vx1 : vx;
+      vy = up != down ? vy1 : vy;
+      const float r1 = rem_euclid(left ? rot - kRotationSpeed : rot + kRotationSpeed, 2.0f * kPi);
+      rot = left != right ? r1 : rot;
     }
-    if (left != right) rot = rem_euclid(left ? rot - kRotationSpeed : rot + kRotationSpeed, 2.0f * kPi);
     speed_clamp(vx, vy);
     float x = old_x + vx, y = old_y + vy;
     x = fminf(fmaxf(x, 0.0f), kWidth);

@@ -379,3 +379,4 @@ def test_run_ticks_fused_mismatch_and_corruption(gpu_available):
     np.testing.assert_array_equal(ei.value.frames, last_frames)
     assert list(np.nonzero(ei.value.frames != -1)[0]) == [5, 33]
     compare_live(sess, orc, G.Game.EX_GAME)
+    compare_cells(sess, orc, P, G.Game.EX_GAME)  # frozen sessions' cells end as after their failing tick

@@ -10,4 +10,5 @@ F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fhip-fp32-corre
 name=$1; shift
 mkdir -p build/var
 /opt/rocm/bin/hipcc $F "$@" -DRB_EXGAME_P2_ONLY=1 -c -o build/var/ex_$name.o ops_exgame.hip
-/opt/rocm/bin/hipcc $F -shared -o ../var/lib_$name.so build/engine.o build/var/ex_$name.o build/ops_brawler.o build/ops_stub.o
+OBJS=$(ls build/*.o | grep -v ops_exgame.o)
+/opt/rocm/bin/hipcc $F -shared -o ../var/lib_$name.so $OBJS build/var/ex_$name.o
