@@ -42,6 +42,16 @@ def algorithmic_bytes_per_session_tick(P: int, cd: int, nw: int, cs_bytes: int, 
     return 4 * nw * (1 + cd) + cd * cs_bytes * 2 + (cd + 1) * P * in_bytes + 4
 
 
+def init_dist(dist, dev):
+    """RCCL over xGMI (backend "nccl"); GGRS_BENCH_BACKEND=gloo rehearses the
+    multi-rank path with several ranks on one GPU (RCCL refuses duplicate GPUs)."""
+    backend = os.environ.get("GGRS_BENCH_BACKEND", "nccl")
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=dev)
+    else:
+        dist.init_process_group(backend)
+
+
 def cpu_baseline(args, P):
     from oracle import oracle as O
     threads = max(1, min(16, os.cpu_count() or 1))
@@ -93,10 +103,11 @@ def bench_p2p(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = local % max(1, torch.cuda.device_count())  # one rank per GPU (ranks share a GPU only in rehearsals)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        init_dist(dist, dev)
     P, S, W = args.num_players, args.sessions_per_gpu, args.max_prediction
     lo, hi = (int(x) for x in args.lag.split(","))
     T = args.warmup + args.steps
@@ -265,10 +276,11 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    local = local % max(1, torch.cuda.device_count())  # one rank per GPU (ranks share a GPU only in rehearsals)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
+        init_dist(dist, dev)  # RCCL over xGMI
 
     P, cd = args.num_players, args.check_distance
     S = args.sessions_per_gpu
