@@ -221,6 +221,18 @@ def bench_p2p(args):
                                                                           else " (fused P2P ticks)")},
             "cpu_baseline": None,
         }
+        if world == 1 and not args.no_cpu_baseline:
+            # the reference rollback path (the oracle's P2PSession + ex_game, reference allocation
+            # pattern) on the same arrays: same inputs, same delivery schedule, same rollbacks
+            from oracle import oracle as O
+            threads = max(1, min(16, os.cpu_count() or 1))
+            secs, cadv, nerr = O.bench_p2p_exgame(P, W, args.input_delay, mask, args.remote_delay, inputs, upto, rin,
+                                                  args.warmup, threads)
+            line["cpu_baseline"] = {
+                "value": cadv / secs, "unit": "session-frames/s", "cores": threads, "kind": "port",
+                "sample": f"the full workload ({S} sessions x {args.steps} timed ticks, {cadv} AdvanceFrames) through "
+                          f"the C++ restatement of P2PSession rollback (no fan-out: the reference has none), "
+                          f"{threads} host threads, {secs:.2f} s wall, {nerr} errors"}
         print(json.dumps(line), flush=True)
     sess.close()
     if world > 1:

@@ -62,6 +62,8 @@ def load():
             "orc_p2p_read_live": (I32, [P, P, P]),
             "orc_p2p_frames": (I32, [P, P, P]),
             "orc_wire_encode": (I32, [P, I32, P, I32, P, I32]),
+            "orc_bench_p2p_exgame": (ctypes.c_double, [I32, I32, I32, ctypes.c_uint32, I32, I32, I32, I32, I32, P,
+                                                        P, P, I32, P, P]),
             "orc_wire_decode": (I32, [P, I32, P, I32, P, I32]),
         }
         for name, (res, args) in sig.items():
@@ -285,3 +287,18 @@ def wire_decode(ref: bytes, data: bytes, cap: int = 4096):
         return None
     assert n >= 0
     return out[:n]
+
+
+def bench_p2p_exgame(P: int, W: int, delay: int, local_mask: int, remote_delay: int, inputs, upto, remote_in,
+                     warmup: int, threads: int):
+    """CPU 'port' baseline of the P2P rollback path on the given synthetic
+    network arrays: (wall seconds of ticks [warmup, T), AdvanceFrames executed, errors)."""
+    T, _, S = inputs.shape
+    a = np.ascontiguousarray(inputs, np.uint8)
+    u = np.ascontiguousarray(upto, np.int32)
+    r = np.ascontiguousarray(remote_in, np.uint8)
+    adv = np.zeros(1, np.int64)
+    ne = np.zeros(1, np.int32)
+    t = load().orc_bench_p2p_exgame(P, W, delay, local_mask, remote_delay, S, T, warmup, threads, _ptr(a), _ptr(u),
+                                    _ptr(r), r.shape[0], _ptr(adv), _ptr(ne))
+    return t, int(adv[0]), int(ne[0])

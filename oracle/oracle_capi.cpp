@@ -595,3 +595,87 @@ double orc_bench_brawler(int32_t num_players, int32_t check_distance, int32_t in
 }
 
 }  // extern "C"
+
+// CPU baseline for the P2P rollback batches: S network-free reference
+// P2PSessions + games (ex_game), driven like ex_game_p2p.rs:105-125 with the
+// delivery schedule bench.py generates (same arrays as the GPU run), split
+// over `threads` host threads.  Returns the wall seconds of ticks
+// [warmup, T); *adv = AdvanceFrames the games executed in that region.
+template <class Cfg, class Game>
+double bench_p2p_game(int32_t P, int32_t W, int32_t delay, uint32_t local_mask, int32_t remote_delay, int32_t S,
+                      int32_t T, int32_t warmup, int32_t threads, const uint8_t* inputs /*[T][P][S]*/,
+                      const int32_t* upto /*[T][P][S]*/, const uint8_t* remote_in /*[F][P][S]*/, int32_t F,
+                      int64_t* adv, int32_t* n_err) {
+  if (threads < 1) threads = 1;
+  std::vector<bool> local(static_cast<size_t>(P));
+  for (int32_t h = 0; h < P; ++h) local[h] = (local_mask >> h) & 1u;
+  struct Worker {
+    std::vector<std::unique_ptr<P2PSession<Cfg>>> sess;
+    std::vector<Game> games;
+    int32_t s0 = 0, s1 = 0, errs = 0;
+    int64_t adv = 0;
+  };
+  std::vector<Worker> ws(threads);
+  for (int32_t t = 0; t < threads; ++t) {
+    ws[t].s0 = static_cast<int32_t>(static_cast<int64_t>(S) * t / threads);
+    ws[t].s1 = static_cast<int32_t>(static_cast<int64_t>(S) * (t + 1) / threads);
+  }
+  auto idx = [&](int32_t f, int32_t h, int32_t s) { return (static_cast<size_t>(f) * P + h) * S + s; };
+  auto run = [&](Worker& w, int32_t t0, int32_t t1, bool count) {
+    std::vector<Request<Cfg>> reqs;
+    for (int32_t t = t0; t < t1; ++t)
+      for (int32_t s = w.s0; s < w.s1; ++s) {
+        auto& ss = *w.sess[s - w.s0];
+        for (int32_t h = 0; h < P; ++h) {
+          if (local[h]) continue;
+          Frame last = ss.local_connect_status[h].last_frame;
+          for (Frame f = last == NULL_FRAME ? remote_delay : last + 1; f <= upto[idx(t, h, s)] && f < F; ++f)
+            ss.deliver_remote_input(h, PlayerInput<typename Cfg::Input>(f, typename Cfg::Input{remote_in[idx(f, h, s)]}));
+        }
+        for (int32_t h = 0; h < P; ++h)
+          if (local[h]) ss.add_local_input(h, typename Cfg::Input{inputs[idx(t, h, s)]});
+        Error e = ss.advance_frame(reqs);
+        if (e.is_err()) {
+          ++w.errs;
+          continue;
+        }
+        if (count)
+          for (auto& r : reqs) w.adv += r.kind == RequestKind::Advance;
+        w.games[s - w.s0].handle_requests(reqs);
+      }
+  };
+  auto parallel = [&](auto fn) {
+    std::vector<std::thread> th;
+    for (int32_t t = 0; t < threads; ++t) th.emplace_back([&, t] { fn(ws[t]); });
+    for (auto& x : th) x.join();
+  };
+  parallel([&](Worker& w) {
+    for (int32_t s = w.s0; s < w.s1; ++s) {
+      w.sess.push_back(std::make_unique<P2PSession<Cfg>>(P, W, false, delay, local));
+      w.games.emplace_back(P);
+    }
+    run(w, 0, warmup, false);
+  });
+  auto t0 = std::chrono::steady_clock::now();
+  parallel([&](Worker& w) { run(w, warmup, T, true); });
+  auto t1 = std::chrono::steady_clock::now();
+  int64_t a = 0;
+  int32_t e = 0;
+  for (auto& w : ws) {
+    a += w.adv;
+    e += w.errs;
+  }
+  if (adv) *adv = a;
+  if (n_err) *n_err = e;
+  return std::chrono::duration<double>(t1 - t0).count();
+}
+
+extern "C" {
+double orc_bench_p2p_exgame(int32_t P, int32_t W, int32_t delay, uint32_t local_mask, int32_t remote_delay, int32_t S,
+                            int32_t T, int32_t warmup, int32_t threads, const uint8_t* inputs, const int32_t* upto,
+                            const uint8_t* remote_in, int32_t F, int64_t* adv, int32_t* n_err) {
+  return bench_p2p_game<exgame::Config, exgame::Game>(P, W, delay, local_mask, remote_delay, S, T, warmup, threads,
+                                                      inputs, upto, remote_in, F, adv, n_err);
+}
+}  // extern "C"
+
