@@ -66,6 +66,8 @@ __device__ __noinline__ SinCos sincosf_large(float y, uint32_t* unexpected) {
   return r;
 }
 
+// kInRange: the caller guarantees |y| < 120 (no out-of-line library path).
+template <bool kInRange = false>
 __device__ __forceinline__ SinCos sincosf_glibc(float y, uint32_t* unexpected) {
   // |y| < pi/4 takes glibc's unreduced branch: reduce_fast yields n = 0 and
   // xr = y exactly there, so one straight-line path serves both.
@@ -94,17 +96,21 @@ __device__ __forceinline__ SinCos sincosf_glibc(float y, uint32_t* unexpected) {
     r.s = y;
     r.c = 1.0f;
   }
-  if (__builtin_expect(top >= abstop12(120.0f), 0)) r = sincosf_large(y, unexpected);
+  if constexpr (!kInRange)
+    if (__builtin_expect(top >= abstop12(120.0f), 0)) r = sincosf_large(y, unexpected);
   return r;
 }
 
 // f32::rem_euclid (r = x % rhs; r < 0 ? r + |rhs| : r).  fmod is exact; for
 // |x| < 2|rhs| it is x or x -/+ rhs (Sterbenz), else the library fmodf (out of line).
 __device__ __noinline__ float fmodf_slow(float x, float y) { return fmodf(x, y); }
+// kInRange: the caller guarantees |x| < 2|rhs|.
+template <bool kInRange = false>
 __device__ __forceinline__ float rem_euclid(float x, float rhs) {
   const float ay = __builtin_fabsf(rhs), ax = __builtin_fabsf(x);
   float r = ax < ay ? x : __builtin_copysignf(ax - ay, x);
-  if (__builtin_expect(!(ax < 2.0f * ay), 0)) r = fmodf_slow(x, rhs);
+  if constexpr (!kInRange)
+    if (__builtin_expect(!(ax < 2.0f * ay), 0)) r = fmodf_slow(x, rhs);
   return r < 0.0f ? r + ay : r;
 }
 

@@ -161,6 +161,7 @@ struct ExGame {
 
   // State::advance (ex_game.rs:259-321) for one player.  Compiled with
   // -ffp-contract=off: every f32 operation rounds exactly as the reference's.
+  template <bool kInRange = false>
   __device__ static void advance_player(uint32_t* w, uint32_t input, uint32_t* unexpected) {
     const float old_x = __uint_as_float(w[0]), old_y = __uint_as_float(w[1]);
     const float old_vx = __uint_as_float(w[2]), old_vy = __uint_as_float(w[3]);
@@ -170,12 +171,12 @@ struct ExGame {
     const bool up = input & 1u, down = input & 2u, left = input & 4u, right = input & 8u;
     {  // thrust (:281-284) / brake (:286-289) and rotation (:291-296) as selects: some lane of
        // every wave needs each of them, so branches only add exec-mask bookkeeping
-      const SinCos sc = sincosf_glibc(rot, unexpected);
+      const SinCos sc = sincosf_glibc<kInRange>(rot, unexpected);
       const float tx = kMovementSpeed * sc.c, ty = kMovementSpeed * sc.s;
       const float vx1 = up ? vx + tx : vx - tx, vy1 = up ? vy + ty : vy - ty;
       vx = up != down ? vx1 : vx;
       vy = up != down ? vy1 : vy;
-      const float r1 = rem_euclid(left ? rot - kRotationSpeed : rot + kRotationSpeed, 2.0f * kPi);
+      const float r1 = rem_euclid<kInRange>(left ? rot - kRotationSpeed : rot + kRotationSpeed, 2.0f * kPi);
       rot = left != right ? r1 : rot;
     }
     speed_clamp(vx, vy);
@@ -189,14 +190,25 @@ struct ExGame {
     w[4] = __float_as_uint(rot);
   }
 
+  template <bool kInRange = false>
   __device__ static void advance(uint32_t (&w)[NWL], InRec rec, int lane, uint32_t disconnected_mask,
                                  uint32_t* unexpected) {
 #pragma unroll
     for (int j = 0; j < kPlayersPerLane; ++j) {
       const int i = kSplit ? lane : j;  // player index
       const uint32_t input = ((disconnected_mask >> i) & 1u) ? 4u : player_input(rec, i);  // Disconnected => 4 (:268)
-      advance_player(&w[5 * j], input, unexpected);
+      advance_player<kInRange>(&w[5 * j], input, unexpected);
     }
+  }
+  // Rotations stay in [0, 2pi] once there (rem_euclid), so a state whose every
+  // |rot| < 12 keeps sincos below 120 and rem_euclid's argument below 4pi for
+  // any number of AdvanceFrames: no out-of-line library paths needed.
+  static constexpr bool kHasRangePath = true;
+  __device__ static bool in_range(const uint32_t (&w)[NWL]) {
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < kPlayersPerLane; ++j) ok &= __builtin_fabsf(__uint_as_float(w[5 * j + 4])) < 12.0f;
+    return ok;
   }
 
   // fletcher16(bincode::serialize(&state)) (ex_game.rs:90-91) from registers:
@@ -300,6 +312,9 @@ struct Brawler {
 
   // State::advance (oracle brawler::State::advance): players, then AI against
   // the players' new positions, then the damage the players took.
+  static constexpr bool kHasRangePath = false;
+  __device__ static bool in_range(const uint32_t (&)[NWL]) { return false; }
+  template <bool = false>
   __device__ static void advance(uint32_t (&w)[NWL], InRec rec, int lane, uint32_t disc, uint32_t*) {
     if (lane < P) {  // phase 1: player `lane` (entity lane, slot 0)
       const uint32_t in = ((disc >> lane) & 1u) ? 0u : (static_cast<uint32_t>(rec) >> (8 * lane)) & 0xFFu;
@@ -424,6 +439,9 @@ struct StubGame {
   static constexpr int kCanonWords = 1;
   __device__ static uint32_t player_input(InRec rec, int p) { return static_cast<uint32_t>(rec >> (32 * p)); }
   // stubs.rs:115-125
+  static constexpr bool kHasRangePath = false;
+  __device__ static bool in_range(const uint32_t (&)[NWL]) { return false; }
+  template <bool = false>
   __device__ static void advance(uint32_t (&w)[NWL], InRec rec, int, uint32_t, uint32_t*) {
     const uint32_t p0 = player_input(rec, 0), p1 = player_input(rec, 1);
     w[0] = ((p0 + p1) % 2u == 0u) ? w[0] + 2u : w[0] - 1u;
@@ -451,6 +469,9 @@ struct StubEnumGame {
   static constexpr int kCanonWords = 1;
   __device__ static uint32_t player_input(InRec rec, int p) { return (static_cast<uint32_t>(rec) >> (8 * p)) & 0xffu; }
   // stubs_enum.rs:206-216
+  static constexpr bool kHasRangePath = false;
+  __device__ static bool in_range(const uint32_t (&)[NWL]) { return false; }
+  template <bool = false>
   __device__ static void advance(uint32_t (&w)[NWL], InRec rec, int, uint32_t, uint32_t*) {
     w[0] = (player_input(rec, 0) == player_input(rec, 1)) ? w[0] + 2u : w[0] - 1u;
   }

@@ -27,6 +27,7 @@
 #include "../../include/ggrs_amd.h"
 #include "games.hpp"
 #include "planner.hpp"
+#include <type_traits>
 
 namespace rb {
 
@@ -434,6 +435,11 @@ __global__ void __launch_bounds__(256) steady_kernel(const RunParams p) {
     int32_t mismatch = kNullFrame;
     CS recorded{};
     uint32_t wn[NW];  // next tick's LoadGameState(c+1-CD), loaded right after this tick saves it
+    // The tick's steps, instantiated twice: with the game's out-of-line range
+    // checks compiled out when the whole wave's loaded state is in range
+    // (G::in_range, decided once per tick), and the general form otherwise.
+    auto steps = [&](auto in_range_tag) __attribute__((always_inline)) {
+    constexpr bool kInRange = decltype(in_range_tag)::value;
 #pragma unroll
     for (int k = 0; k <= CD; ++k) {
       const int f = f0 + k;
@@ -456,14 +462,19 @@ __global__ void __launch_bounds__(256) steady_kernel(const RunParams p) {
       if (dbg & 1u)
         w[0] += win[k];
       else
-        G::advance(w, (dbg & 32u) ? static_cast<InRec>(win[k] & static_cast<InRec>(dbg >> 8)) : win[k], lane, 0u,
-                   &p.counters[1]);  // AdvanceFrame{inputs}
+        G::template advance<kInRange>(w, (dbg & 32u) ? static_cast<InRec>(win[k] & static_cast<InRec>(dbg >> 8)) : win[k],
+                                      lane, 0u, &p.counters[1]);  // AdvanceFrame{inputs}
       if ((f + 1) % 100 == 0) {  // ex_game periodic_checksum (frame % CHECKSUM_PERIOD == 0)
         ctx.nonce = nonce + 128u + static_cast<uint32_t>(k);
         const CS cval = G::checksum(w, f + 1, lane, ctx);
         if (G::kDisplay && lead) reinterpret_cast<CS*>(p.periodic_cs)[s] = cval;
       }
     }
+    };
+    if (G::kHasRangePath && __all(G::in_range(w)))
+      steps(std::true_type{});
+    else
+      steps(std::false_type{});
     if constexpr (G::kDisplay) {  // Game::last_checksum after the final AdvanceFrame
       ctx.nonce = nonce + 255u;
       const CS cval = G::checksum(w, c + 1, lane, ctx);
