@@ -619,7 +619,7 @@ struct GameOpsT final : GameOps {
   }
   hipError_t launch_p2p(const P2PParams& p, int block, hipStream_t st) const override {
     const int grid = (p.Spad * G::kLanes + block - 1) / block;
-    hipLaunchKernelGGL(p2p_kernel<G>, dim3(grid), dim3(block), 0, st, p);
+    hipLaunchKernelGGL(p2p_kernel<G>, dim3(grid), dim3(block), p2p_lds_bytes<G>(block), st, p);
     return hipGetLastError();
   }
   static constexpr bool kFanout = G::kLanes > 1 && G::kLanes <= 4;

@@ -133,9 +133,33 @@ struct RingIO {
   }
 };
 
+// The same ring in LDS, for a kernel whose lanes own one player each
+// (p2p_lds_queue below): column = thread, row = frame % 128.  p2p_kernel
+// copies in the HBM frames a launch can read and writes back the frames it
+// adds.  Inside the launch an input read is an LDS read: LDS has its own
+// counter, so it never waits for the tick's snapshot stores the way a global
+// load issued after them does (vmcnt retires loads and stores in order).
+struct LdsRing {
+  uint8_t* col;       // this thread's column: lds + threadIdx.x
+  unsigned row;       // bytes per frame row (blockDim.x)
+  __device__ uint32_t get(int32_t f, int, unsigned) const { return col[static_cast<unsigned>(f & (kQueueLen - 1)) * row]; }
+  __device__ void put(int32_t f, int, unsigned, uint32_t v) const {
+    col[static_cast<unsigned>(f & (kQueueLen - 1)) * row] = static_cast<uint8_t>(v);
+  }
+};
+// LDS queues: 1-byte inputs, one player per lane (ex_game lane per player, the brawler).
+template <class G>
+constexpr bool p2p_lds_queue() {
+  return G::kInputBytes == 1 && (G::kLanes > 1 || G::kPlayers == 1);
+}
+template <class G>
+constexpr size_t p2p_lds_bytes(int block) {
+  return p2p_lds_queue<G>() ? static_cast<size_t>(kQueueLen) * static_cast<size_t>(block) : 0;
+}
+
 // input_queue.rs:167-204 add_input_by_frame
-template <int IB>
-__device__ __forceinline__ void q_add_by_frame(DevQueue& q, const RingIO<IB>& r, int h, unsigned s, int32_t f, uint32_t v) {
+template <class R>
+__device__ __forceinline__ void q_add_by_frame(DevQueue& q, const R& r, int h, unsigned s, int32_t f, uint32_t v) {
   r.put(f, h, s, v);
   q.last_added = f;
   if (q.pred_frame != kNullFrame) {
@@ -146,8 +170,8 @@ __device__ __forceinline__ void q_add_by_frame(DevQueue& q, const RingIO<IB>& r,
 }
 // input_queue.rs:149-163 + 207-239 add_input with the delay already applied to
 // `f`: replicate the entry before head (blank before the first add) up to f.
-template <int IB>
-__device__ __forceinline__ int32_t q_add(DevQueue& q, const RingIO<IB>& r, int h, unsigned s, int32_t f, uint32_t v) {
+template <class R>
+__device__ __forceinline__ int32_t q_add(DevQueue& q, const R& r, int h, unsigned s, int32_t f, uint32_t v) {
   int32_t expected = q.last_added == kNullFrame ? 0 : q.last_added + 1;
   if (expected > f) return kNullFrame;
   const uint32_t rep = q.last_added == kNullFrame ? 0u : r.get(q.last_added, h, s);
@@ -156,8 +180,8 @@ __device__ __forceinline__ int32_t q_add(DevQueue& q, const RingIO<IB>& r, int h
   return f;
 }
 // input_queue.rs:104-146 input(requested_frame)
-template <int IB>
-__device__ __forceinline__ uint32_t q_input(DevQueue& q, const RingIO<IB>& r, int h, unsigned s, int32_t f) {
+template <class R>
+__device__ __forceinline__ uint32_t q_input(DevQueue& q, const R& r, int h, unsigned s, int32_t f) {
   q.last_req = f;
   if (q.pred_frame < 0) {
     if (q.last_added != kNullFrame && f <= q.last_added) return r.get(f, h, s);  // Confirmed
@@ -190,7 +214,13 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
   const unsigned slot_words = static_cast<unsigned>(NW) * Gpad;
   const int W = p.W;
   CS* __restrict__ csa = reinterpret_cast<CS*>(p.cs);
-  const RingIO<IB> ring{reinterpret_cast<uint8_t*>(p.ring), P, p.Spad};
+  constexpr bool kLdsQ = p2p_lds_queue<G>();
+  const RingIO<IB> hbm{reinterpret_cast<uint8_t*>(p.ring), P, p.Spad};
+  extern __shared__ uint8_t lds_queue[];
+  const auto ring = [&]() __attribute__((always_inline)) {
+    if constexpr (kLdsQ) return LdsRing{lds_queue + threadIdx.x, blockDim.x};
+    else return hbm;
+  }();
   auto qrow = [&](int field, int h) __attribute__((always_inline)) { return p.qs + static_cast<size_t>(QS_PLAYER0 + field * 4 + h) * Spad + s; };
   auto player_of = [&](int j) __attribute__((always_inline)) { return kSplit ? lane : j; };
 
@@ -214,6 +244,25 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
   }
   uint32_t w[NW];
   load_words<NW>(p.live, static_cast<int>(Gpad), static_cast<int>(g), w);
+  // LDS queue: the HBM frames this launch can read.  Reads are of frames
+  // >= cur - W (adjust_gamestate checks that before it advances) up to the
+  // last added one, or of the last added frame itself (predictions and the
+  // delay replication); every later frame is added inside the launch.
+  const int32_t la0 = q[0].last_added;
+  if constexpr (kLdsQ) {
+    const int h = player_of(0);
+    if (h < P && la0 != kNullFrame) {
+      const int32_t lo = max(max(0, la0 - (kQueueLen - 1)), min(cur - W, la0));
+      for (int32_t f0 = lo; f0 <= la0; f0 += 8) {  // 8 loads in flight per round trip
+        uint32_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = hbm.get(min(f0 + k, la0), h, s);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (f0 + k <= la0) ring.put(f0 + k, h, s, v[k]);
+      }
+    }
+  }
 
   int32_t status = kP2PStatusOk, load_frame = kNullFrame, nadv = 0, nsave = 0;
   uint32_t nonce = 0;
@@ -245,7 +294,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
 #pragma unroll
     for (int j = 0; j < PPL; ++j) {
       const int h = player_of(j);
-      if (h < P) rec |= static_cast<uint64_t>(q_input<IB>(q[j], ring, h, s, f)) << (8 * IB * h);
+      if (h < P) rec |= static_cast<uint64_t>(q_input(q[j], ring, h, s, f)) << (8 * IB * h);
     }
     return static_cast<InRec>(rec);
   };
@@ -365,21 +414,80 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     last_conf = p.sparse ? min(confirmed, last_saved) : confirmed;  // set_last_confirmed_frame (sync_layer.rs:220-244)
   };
 
+  // ---- the per-tick delivery tensors, loaded one tick ahead: at the top of
+  // tick t, before its snapshot stores, come the delivered watermark and the
+  // local inputs of tick t+1; right after the poll, the first kPre remote
+  // frames tick t+1 will add (their frame numbers are known once the poll
+  // has moved the connection status).  Every lane loads (clamped, always
+  // valid addresses) and uses what its players need: a branch around a load
+  // would make the compiler wait for it at the join.
+  constexpr int kPre = 4;
+  const int first_local = p.local_mask ? __builtin_ctz(p.local_mask) : 0;
+  auto load_upto = [&](int t, int j) __attribute__((always_inline)) -> int32_t {
+    const int h = min(player_of(j), P - 1);
+    return p.upto[static_cast<int64_t>(t) * p.upto_stride + static_cast<int64_t>(h) * p.S + s];
+  };
+  auto load_local = [&](int t, int j) __attribute__((always_inline)) -> uint32_t {
+    if (!p.local_mask) return 0u;  // launch-uniform
+    int h = player_of(j);
+    h = (h < P && ((p.local_mask >> h) & 1u)) ? h : first_local;
+    const uint8_t* src = p.local_in + static_cast<int64_t>(t) * p.local_stride + (static_cast<size_t>(h) * p.S + s) * IB;
+    return IB == 4 ? *reinterpret_cast<const uint32_t*>(src) : *src;
+  };
+  auto remote_start = [&](int j) __attribute__((always_inline)) {
+    return q[j].conn_last == kNullFrame ? p.remote_delay : q[j].conn_last + 1;
+  };
+  auto load_remote = [&](int j, int32_t f) __attribute__((always_inline)) -> uint32_t {
+    const int h = min(player_of(j), P - 1);
+    f = max(0, min(f, p.remote_frames - 1));
+    const uint8_t* src = p.remote_in + (static_cast<size_t>(f) * P + h) * p.S * IB + static_cast<size_t>(s) * IB;
+    return IB == 4 ? *reinterpret_cast<const uint32_t*>(src) : *src;
+  };
+  int32_t up[PPL];
+  uint32_t lin[PPL], rv[PPL][kPre];
+#pragma unroll
+  for (int j = 0; j < PPL; ++j) {
+    up[j] = load_upto(0, j);
+    lin[j] = load_local(0, j);
+    const int32_t f = remote_start(j);
+#pragma unroll
+    for (int k = 0; k < kPre; ++k) rv[j][k] = load_remote(j, f + k);
+  }
+
   for (int t = 0; t < p.T; ++t) {
+    const int tn = t + 1 < p.T ? t + 1 : t;
+    int32_t up_n[PPL];
+    uint32_t lin_n[PPL], rv_n[PPL][kPre];
+#pragma unroll
+    for (int j = 0; j < PPL; ++j) {
+      up_n[j] = load_upto(tn, j);
+      lin_n[j] = load_local(tn, j);
+    }
     status = kP2PStatusOk;
     // ---- poll_remote_clients: Event::Input in frame order (handle_event, :838-852)
 #pragma unroll
     for (int j = 0; j < PPL; ++j) {
       const int h = player_of(j);
-      if (h >= P || ((p.local_mask >> h) & 1u)) continue;
-      const int32_t up = p.upto[static_cast<int64_t>(t) * p.upto_stride + static_cast<int64_t>(h) * p.S + s];
-      int32_t f = q[j].conn_last == kNullFrame ? p.remote_delay : q[j].conn_last + 1;
-      for (; f <= up && f < p.remote_frames; ++f) {
-        const uint8_t* src = p.remote_in + (static_cast<size_t>(f) * P + h) * p.S * IB + static_cast<size_t>(s) * IB;
-        const uint32_t v = IB == 4 ? *reinterpret_cast<const uint32_t*>(src) : *src;
-        q_add<IB>(q[j], ring, h, s, f, v);  // add_remote_input (frame delay 0)
-        q[j].conn_last = f;
+      if (h < P && !((p.local_mask >> h) & 1u)) {
+        const int32_t end = min(up[j], p.remote_frames - 1);
+        int32_t f = remote_start(j);
+#pragma unroll
+        for (int k = 0; k < kPre; ++k, ++f) {
+          if (f > end) break;
+          q_add(q[j], ring, h, s, f, rv[j][k]);  // add_remote_input (frame delay 0)
+          q[j].conn_last = f;
+        }
+        for (; f <= end; ++f) {  // more than kPre frames delivered in one tick
+          q_add(q[j], ring, h, s, f, load_remote(j, f));
+          q[j].conn_last = f;
+        }
       }
+    }
+#pragma unroll
+    for (int j = 0; j < PPL; ++j) {
+      const int32_t f = remote_start(j);
+#pragma unroll
+      for (int k = 0; k < kPre; ++k) rv_n[j][k] = load_remote(j, f + k);
     }
     // ---- PredictionThreshold (sync_layer.rs:163-167) is decided by bookkeeping
     // alone: without sparse saving from the confirmed frame, with it by a dry run.
@@ -417,24 +525,36 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
       load_frame = kNullFrame;       // and the user never sees the dropped requests
       nadv = nsave = 0;
       if (lead) atomicAdd(&p.counters[0], 1u);
-      continue;
+    } else {
+      rollback_and_save();
+      if (status == kP2PStatusPanic) break;
+      // ---- local inputs: SyncLayer::add_local_input (sync_layer.rs:159-174)
+#pragma unroll
+      for (int j = 0; j < PPL; ++j) {
+        const int h = player_of(j);
+        if (h >= P || !((p.local_mask >> h) & 1u)) continue;
+        q[j].conn_last = q_add(q[j], ring, h, s, cur + p.delay, lin[j]);  // local_connect_status[h].last_frame
+      }
+      advance(cur);
+      cur += 1;
     }
-    rollback_and_save();
-    if (status == kP2PStatusPanic) break;
-    // ---- local inputs: SyncLayer::add_local_input (sync_layer.rs:159-174)
 #pragma unroll
     for (int j = 0; j < PPL; ++j) {
-      const int h = player_of(j);
-      if (h >= P || !((p.local_mask >> h) & 1u)) continue;
-      const uint8_t* src = p.local_in + static_cast<int64_t>(t) * p.local_stride +
-                           (static_cast<size_t>(h) * p.S + s) * IB;
-      const uint32_t v = IB == 4 ? *reinterpret_cast<const uint32_t*>(src) : *src;
-      q[j].conn_last = q_add<IB>(q[j], ring, h, s, cur + p.delay, v);  // local_connect_status[h].last_frame
+      up[j] = up_n[j];
+      lin[j] = lin_n[j];
+#pragma unroll
+      for (int k = 0; k < kPre; ++k) rv[j][k] = rv_n[j][k];
     }
-    advance(cur);
-    cur += 1;
   }
 
+  // ---- LDS queue: the frames added in this launch back to the HBM ring
+  if constexpr (kLdsQ) {
+    const int h = player_of(0);
+    const int32_t la = q[0].last_added;
+    if (h < P && la != kNullFrame) {
+      for (int32_t f = max(la0 == kNullFrame ? 0 : la0 + 1, la - (kQueueLen - 1)); f <= la; ++f) hbm.put(f, h, s, ring.get(f, h, s));
+    }
+  }
   // ---- write back
   store_words<NW>(p.live, static_cast<int>(Gpad), static_cast<int>(g), w);
 #pragma unroll
