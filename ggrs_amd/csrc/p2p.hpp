@@ -39,7 +39,8 @@ enum : int {
   QS_CUR = 0,         // SyncLayer::current_frame
   QS_LAST_SAVED = 1,  // SyncLayer::last_saved_frame
   QS_LAST_CONF = 2,   // SyncLayer::last_confirmed_frame
-  QS_PLAYER0 = 3,     // + field * 4 + player (4 player slots)
+  QS_DISC_FRAME = 3,  // P2PSession::disconnect_frame (p2p_session.rs:130)
+  QS_PLAYER0 = 4,     // + field * 4 + player (4 player slots)
 };
 enum : int {
   QF_LAST_ADDED = 0,   // InputQueue::last_added_frame
@@ -48,7 +49,8 @@ enum : int {
   QF_FIRST_INC = 3,    // InputQueue::first_incorrect_frame
   QF_LAST_REQ = 4,     // InputQueue::last_requested_frame
   QF_CONN_LAST = 5,    // ConnectionStatus::last_frame (messages.rs:5-18)
-  QF_COUNT = 6,
+  QF_DISC = 6,         // ConnectionStatus::disconnected (0 / 1)
+  QF_COUNT = 7,
 };
 constexpr int kQsFields = QS_PLAYER0 + QF_COUNT * 4;
 // trace rows (the last tick of the last launch): LoadGameState frame, AdvanceFrame count, SaveGameState count
@@ -115,6 +117,7 @@ __device__ __forceinline__ int32_t group_min(int32_t v) {
 struct DevQueue {
   int32_t last_added, pred_frame, first_inc, last_req, conn_last;
   uint32_t pred_val;
+  bool disc;  // ConnectionStatus::disconnected: set between launches only (rb_p2p_disconnect_player)
 };
 
 template <int IB>
@@ -238,10 +241,20 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
       q[j].first_inc = *qrow(QF_FIRST_INC, h);
       q[j].last_req = *qrow(QF_LAST_REQ, h);
       q[j].conn_last = *qrow(QF_CONN_LAST, h);
+      q[j].disc = *qrow(QF_DISC, h) != 0;
     } else {  // padding lane of a 4-lane group (P = 3): no player
-      q[j] = DevQueue{kNullFrame, kNullFrame, kNullFrame, kNullFrame, INT32_MAX, 0u};
+      q[j] = DevQueue{kNullFrame, kNullFrame, kNullFrame, kNullFrame, INT32_MAX, 0u, false};
     }
   }
+  // disconnect_player between launches: P2PSession::disconnect_frame, consumed
+  // by the next advance_frame's check_simulation_consistency (:281-288)
+  int32_t disc_frame = p.qs[QS_DISC_FRAME * Spad + s];
+  bool any_disc = false;
+#pragma unroll
+  for (int j = 0; j < PPL; ++j) any_disc |= q[j].disc;
+  any_disc = group_min<L>(any_disc ? 0 : 1) == 0;
+  // confirmed_frame (:487-498) skips disconnected players
+  auto conn_of = [&](int j) __attribute__((always_inline)) { return q[j].disc ? INT32_MAX : q[j].conn_last; };
   uint32_t w[NW];
   load_words<NW>(p.live, static_cast<int>(Gpad), static_cast<int>(g), w);
   // LDS queue: the HBM frames this launch can read.  Reads are of frames
@@ -288,21 +301,26 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
       p.tag[slot * Spad + s] = f;
     }
   };
-  // SyncLayer::synchronized_inputs (sync_layer.rs:187-200) for this lane's players
-  auto sync_inputs = [&](int32_t f) __attribute__((always_inline)) -> InRec {
+  // SyncLayer::synchronized_inputs (sync_layer.rs:187-200) for this lane's
+  // players: a disconnected player past its last frame is (zeroed, Disconnected)
+  // and its queue is not asked
+  auto sync_inputs = [&](int32_t f, uint32_t& dmask) __attribute__((always_inline)) -> InRec {
     uint64_t rec = 0;
 #pragma unroll
     for (int j = 0; j < PPL; ++j) {
       const int h = player_of(j);
-      if (h < P) rec |= static_cast<uint64_t>(q_input(q[j], ring, h, s, f)) << (8 * IB * h);
+      if (h >= P) continue;
+      if (q[j].disc && q[j].conn_last < f) dmask |= 1u << h;
+      else rec |= static_cast<uint64_t>(q_input(q[j], ring, h, s, f)) << (8 * IB * h);
     }
     return static_cast<InRec>(rec);
   };
   auto advance = [&](int32_t f) __attribute__((always_inline)) {  // AdvanceFrame{inputs}
-    const InRec rec = sync_inputs(f);
+    uint32_t dmask = 0u;
+    const InRec rec = sync_inputs(f, dmask);
     ++nadv;
     if (exec) {
-      G::advance(w, rec, lane, 0u, &p.counters[1]);
+      G::advance(w, rec, lane, dmask, &p.counters[1]);
       ++tot_adv;
     }
   };
@@ -311,7 +329,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     const int32_t to_load = p.sparse ? last_saved : first_incorrect;
     const int32_t count = cur - to_load;
     const unsigned slot = static_cast<unsigned>(to_load % W);
-    if (to_load < 0 || to_load > first_incorrect || count > W || p.tag[slot * Spad + s] != to_load) {
+    if (to_load < 0 || to_load > first_incorrect || count <= 0 || count > W || p.tag[slot * Spad + s] != to_load) {
       status = kP2PStatusPanic;  // a reference assert (sync_layer.rs:141-148) would fire
       return;
     }
@@ -342,6 +360,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
   // predictions for the others, confirmed local inputs).  The sync layer's
   // bookkeeping runs as in adjust (dry), the cells and the state are copied.
   auto try_select = [&](int32_t first_incorrect, int32_t min_confirmed) __attribute__((always_inline)) -> bool {
+    if (any_disc || disc_frame != kNullFrame) return false;  // the branches assumed everybody connected
     if (!p.spec_meta[SM_VALID * Spad + s] || p.spec_meta[SM_END * Spad + s] != cur) return false;
     const int32_t base = p.spec_meta[SM_BASE * Spad + s];
     const int rs = p.spec_meta[SM_PLAYER * Spad + s];
@@ -396,12 +415,16 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     int32_t confirmed = INT32_MAX, first_inc = INT32_MAX;
 #pragma unroll
     for (int j = 0; j < PPL; ++j) {
-      confirmed = min(confirmed, q[j].conn_last);  // confirmed_frame (:487-498)
+      confirmed = min(confirmed, conn_of(j));  // confirmed_frame (:487-498)
       if (q[j].first_inc != kNullFrame) first_inc = min(first_inc, q[j].first_inc);  // check_simulation_consistency
     }
     confirmed = group_min<L>(confirmed);
     first_inc = group_min<L>(first_inc);
-    if (first_inc != INT32_MAX && !(p.spec_on && exec && try_select(first_inc, confirmed))) adjust(first_inc, confirmed);
+    if (disc_frame != kNullFrame) first_inc = min(first_inc, disc_frame);  // session-uniform
+    if (first_inc != INT32_MAX) {
+      if (!(p.spec_on && exec && try_select(first_inc, confirmed))) adjust(first_inc, confirmed);
+      disc_frame = kNullFrame;
+    }
     if (status == kP2PStatusPanic) return;
     if (p.sparse) {  // check_last_saved_state (:778-802)
       if (cur - last_saved >= W) {
@@ -468,7 +491,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
 #pragma unroll
     for (int j = 0; j < PPL; ++j) {
       const int h = player_of(j);
-      if (h < P && !((p.local_mask >> h) & 1u)) {
+      if (h < P && !((p.local_mask >> h) & 1u) && !q[j].disc) {  // handle_event ignores a disconnected player (:852)
         const int32_t end = min(up[j], p.remote_frames - 1);
         int32_t f = remote_start(j);
 #pragma unroll
@@ -495,7 +518,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     if (!p.sparse) {
       int32_t confirmed = INT32_MAX;
 #pragma unroll
-      for (int j = 0; j < PPL; ++j) confirmed = min(confirmed, q[j].conn_last);
+      for (int j = 0; j < PPL; ++j) confirmed = min(confirmed, conn_of(j));
       confirmed = group_min<L>(confirmed);
       threshold = cur >= W && cur - confirmed >= W;
       if (threshold) {
@@ -504,7 +527,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
         exec = true;
       }
     } else {
-      const int32_t cur0 = cur, ls0 = last_saved;
+      const int32_t cur0 = cur, ls0 = last_saved, df0 = disc_frame;
       DevQueue q0[PPL];
 #pragma unroll
       for (int j = 0; j < PPL; ++j) q0[j] = q[j];
@@ -515,6 +538,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
       if (!threshold && status != kP2PStatusPanic) {
         cur = cur0;
         last_saved = ls0;
+        disc_frame = df0;
 #pragma unroll
         for (int j = 0; j < PPL; ++j) q[j] = q0[j];
       }
@@ -572,6 +596,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     p.qs[QS_CUR * Spad + s] = cur;
     p.qs[QS_LAST_SAVED * Spad + s] = last_saved;
     p.qs[QS_LAST_CONF * Spad + s] = last_conf;
+    p.qs[QS_DISC_FRAME * Spad + s] = disc_frame;
     p.status[s] = status;
     p.trace[TR_LOAD * Spad + s] = load_frame;
     p.trace[TR_NADV * Spad + s] = nadv;
@@ -645,8 +670,11 @@ __global__ void __launch_bounds__(256) fanout_kernel(const FanParams p) {
       rs = h;
     }
   }
+  bool any_disc = false;
+#pragma unroll
+  for (int h = 0; h < P; ++h) any_disc |= qrow(QF_DISC, h) != 0;
   const int32_t base = la_rs + 1;  // first unconfirmed frame of the speculated player
-  const bool valid = rs >= 0 && base < cur && base + W > cur && base >= 0 &&
+  const bool valid = !any_disc && rs >= 0 && base < cur && base + W > cur && base >= 0 &&
                      p.tag[static_cast<unsigned>(base % W) * Spad + s] == base;
   if (k == 0 && lane == 0) {
     p.spec_meta[SM_BASE * Spad + s] = base;

@@ -30,6 +30,8 @@ struct rb_p2p {
   uint32_t* spec_cells = nullptr;
   void* spec_cs = nullptr;
   int32_t* spec_meta = nullptr;
+  std::vector<uint8_t> disconnected;  // host mirror [P][S] of ConnectionStatus::disconnected (validation)
+  uint8_t* disc_mask = nullptr;       // [S] device copy of rb_p2p_disconnect_player's session mask
   bool prof = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev;
   size_t prof_used = 0;
@@ -54,7 +56,8 @@ void free_all(rb_p2p* b) {
   (void)hipSetDevice(b->device);
   if (b->stream) (void)hipStreamSynchronize(b->stream);
   void* ptrs[] = {b->snap,   b->cs,      b->tag,       b->ring,       b->live,    b->qs,       b->status,
-                  b->trace,  b->counters, b->stats, b->spec_state, b->spec_cells, b->spec_cs, b->spec_meta};
+                  b->trace,  b->counters, b->stats, b->spec_state, b->spec_cells, b->spec_cs, b->spec_meta,
+                  b->disc_mask};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   for (auto& pr : b->prof_ev) {
@@ -73,6 +76,18 @@ rb_status read_rows(rb_p2p* b, const T* dev, size_t rows, std::vector<T>& host) 
 }
 
 // session s's words [lanes][nw] from a block of lane planes, as its canonical image
+// disconnect_player_at_frame (p2p_session.rs:555-581) for one remote handle:
+// mark it disconnected and, if the session already simulated past its last
+// input, set disconnect_frame = last_frame + 1
+__global__ void p2p_disconnect_kernel(int32_t* qs, const uint8_t* mask, int32_t S, int32_t Spad, int32_t h) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= S || (mask && !mask[s])) return;
+  const size_t sp = static_cast<size_t>(Spad);
+  const int32_t last = qs[(QS_PLAYER0 + QF_CONN_LAST * 4 + h) * sp + s];
+  qs[(QS_PLAYER0 + QF_DISC * 4 + h) * sp + s] = 1;
+  if (qs[QS_CUR * sp + s] > last) qs[QS_DISC_FRAME * sp + s] = last + 1;
+}
+
 void image_from_planes(const rb_p2p* b, const std::vector<uint32_t>& planes, int s, int32_t frame, uint8_t* out) {
   const int L = b->ops->lanes, NW = b->ops->nw;
   std::vector<uint32_t> w(static_cast<size_t>(L) * NW);
@@ -184,8 +199,13 @@ rb_status rb_p2p_create(const rb_p2p_config* cfg, rb_p2p** out) {
   std::vector<int32_t> qs(kQsFields * Sp, kNullFrame);
   for (size_t s = 0; s < Sp; ++s) {
     qs[QS_CUR * Sp + s] = 0;
-    for (int h = 0; h < 4; ++h) qs[(QS_PLAYER0 + QF_PRED_VAL * 4 + h) * Sp + s] = 0;
+    for (int h = 0; h < 4; ++h) {
+      qs[(QS_PLAYER0 + QF_PRED_VAL * 4 + h) * Sp + s] = 0;
+      qs[(QS_PLAYER0 + QF_DISC * 4 + h) * Sp + s] = 0;  // ConnectionStatus::default: connected
+    }
   }
+  b->disconnected.assign(static_cast<size_t>(b->P) * b->S, 0);
+  P2P_CREATE(hipMalloc(&b->disc_mask, Sp));
   P2P_CREATE(hipMemcpyAsync(b->qs, qs.data(), qs.size() * 4, hipMemcpyHostToDevice, b->stream));
   // State::new for every session
   std::vector<uint32_t> w0(L * NW), planes(NW * Gp);
@@ -296,6 +316,26 @@ rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs,
   }
   if (e != hipSuccess) return pfail(b, RB_DEVICE_ERROR, std::string("p2p launch: ") + hipGetErrorString(e));
   if (b->prof) P2P_TRY(b, hipEventRecord(e1, b->stream));
+  return RB_OK;
+}
+
+rb_status rb_p2p_disconnect_player(rb_p2p* b, int32_t handle, const uint8_t* session_mask) {
+  if (handle < 0 || handle >= b->P) return pfail(b, RB_INVALID_REQUEST, "Invalid Player Handle.");
+  if ((b->cfg.local_mask >> handle) & 1u) return pfail(b, RB_INVALID_REQUEST, "Local Player cannot be disconnected.");
+  uint8_t* d = b->disconnected.data() + static_cast<size_t>(handle) * b->S;
+  for (int s = 0; s < b->S; ++s)
+    if ((!session_mask || session_mask[s]) && d[s]) return pfail(b, RB_INVALID_REQUEST, "Player already disconnected.");
+  for (int s = 0; s < b->S; ++s)
+    if (!session_mask || session_mask[s]) d[s] = 1;
+  P2P_TRY(b, hipSetDevice(b->device));
+  if (session_mask) {
+    P2P_TRY(b, hipMemcpyAsync(b->disc_mask, session_mask, b->S, hipMemcpyHostToDevice, b->stream));
+    P2P_TRY(b, hipStreamSynchronize(b->stream));  // the host mask may be reused as soon as we return
+  }
+  const int blocks = (b->S + 255) / 256;
+  hipLaunchKernelGGL(p2p_disconnect_kernel, dim3(blocks), dim3(256), 0, b->stream, b->qs,
+                     session_mask ? b->disc_mask : nullptr, b->S, b->Spad, handle);
+  P2P_TRY(b, hipGetLastError());
   return RB_OK;
 }
 

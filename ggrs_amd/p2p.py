@@ -17,7 +17,7 @@ import enum
 import numpy as np
 
 from . import _lib as L
-from .session import INPUT_DTYPE, DeviceError, Panic
+from .session import INPUT_DTYPE, DeviceError, InvalidRequest, Panic
 from .synth import SEED, splitmix64
 
 
@@ -96,6 +96,20 @@ class P2PSession:
         self._keep = [lk, uk, rk]
         stride = self.num_players * self.num_sessions * lk.element_size()
         self._check(self._lib.rb_p2p_run_ticks(self._h, T, lp, stride, up, rp, int(remote_inputs.shape[0])))
+
+    def disconnect_player(self, handle: int, sessions=None) -> None:
+        """P2PSession::disconnect_player(handle) (p2p_session.rs:430-456) in every
+        session where `sessions` is true (None: all), between ticks.  Raises
+        InvalidRequest like the reference (invalid handle, local player, already
+        disconnected) and then applies nothing."""
+        m = None
+        if sessions is not None:
+            m = np.ascontiguousarray(np.broadcast_to(np.asarray(sessions), (self.num_sessions,)), dtype=np.uint8)
+        st = self._lib.rb_p2p_disconnect_player(self._h, int(handle),
+                                               None if m is None else m.ctypes.data_as(ctypes.c_void_p))
+        if st == L.RB_INVALID_REQUEST:
+            raise InvalidRequest((self._lib.rb_p2p_last_error(self._h) or b"").decode())
+        self._check(st)
 
     def advance_frame(self, local_inputs, remote_upto, remote_inputs) -> None:
         """One tick (run_ticks with T = 1): local_inputs [P, S], remote_upto [P, S]."""

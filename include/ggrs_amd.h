@@ -207,7 +207,8 @@ rb_status rb_profile_take(rb_batch* b, double* total_ms, int32_t* launches);
  * caller's: per tick and remote handle it passes the newest delivered frame
  * (`remote_upto`) and the inputs by frame (`remote_inputs`).  Mispredicted
  * remote inputs roll sessions back individually (per-session depth), on the
- * device.  Spectators, time sync and disconnects are out of scope.
+ * device.  rb_p2p_disconnect_player covers disconnects the user issues;
+ * spectators, time sync and peer-reported disconnects are out of scope.
  * ======================================================================== */
 typedef struct rb_p2p rb_p2p;
 
@@ -262,6 +263,17 @@ rb_status rb_p2p_set_stream(rb_p2p* b, void* hip_stream);
  * stops and reports RB_PANIC through rb_p2p_read_status / rb_p2p_counters. */
 rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs, int64_t local_stride_bytes,
                            const int32_t* remote_upto, const void* remote_inputs, int32_t remote_frames);
+
+/* P2PSession::disconnect_player(handle) (p2p_session.rs:430-456, 555-581) in
+ * every session whose `session_mask` byte is non-zero (NULL: all sessions),
+ * called between rb_p2p_run_ticks calls (stream ordered).  Errors as the
+ * reference, RB_INVALID_REQUEST with nothing applied: "Invalid Player Handle."
+ * (handle >= num_players), "Local Player cannot be disconnected.", "Player
+ * already disconnected." (in any selected session).  From then on the player's
+ * deliveries are ignored, it leaves the confirmed frame, every frame after its
+ * last one advances with (zeroed, Disconnected), and the next advance_frame
+ * resimulates from last_frame + 1 if that frame was already simulated. */
+rb_status rb_p2p_disconnect_player(rb_p2p* b, int32_t handle, const uint8_t* session_mask);
 
 /* Per session, the last tick: rb_status of its advance_frame, the LoadGameState
  * frame (RB_NULL_FRAME: no rollback), AdvanceFrame and SaveGameState counts.

@@ -482,7 +482,8 @@ class SyncTestSession {
 // caller delivers those inputs directly (deliver_remote_input).  Spectators,
 // time sync / wait recommendations, desync-report messages and the
 // synchronisation handshake (the session starts Running) are out of scope
-// (DESIGN.md §7); disconnects are not modelled (disconnect_frame stays NULL).
+// (DESIGN.md §7).  disconnect_player (a user call between advance_frames) is
+// modelled; update_player_disconnects (peers' connect-status reports) is network.
 // ---------------------------------------------------------------------------
 template <class C>
 class P2PSession {
@@ -520,6 +521,18 @@ class P2PSession {
       local_connect_status[player].last_frame = input.frame;
       sync_layer.add_remote_input(player, input);
     }
+  }
+
+  // :430-456 disconnect_player + :555-581 disconnect_player_at_frame (a remote
+  // handle maps to its own endpoint: one handle per address in the batch)
+  Error disconnect_player(PlayerHandle h) {
+    if (h >= num_players) return Error::invalid("Invalid Player Handle.");
+    if (is_local[h]) return Error::invalid("Local Player cannot be disconnected.");
+    if (local_connect_status[h].disconnected) return Error::invalid("Player already disconnected.");
+    Frame last_frame = local_connect_status[h].last_frame;
+    local_connect_status[h].disconnected = true;
+    if (sync_layer.current_frame() > last_frame) disconnect_frame = last_frame + 1;
+    return Error::ok();
   }
 
   Frame confirmed_frame() const {  // :487-498

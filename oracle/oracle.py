@@ -57,6 +57,7 @@ def load():
             "orc_p2p_deliver": (I32, [P, I32, P, P, I32]),
             "orc_p2p_add_local_input": (I32, [P, I32, P]),
             "orc_p2p_advance": (I32, [P, P, P, P, P]),
+            "orc_p2p_disconnect": (I32, [P, I32, P]),
             "orc_p2p_trace": (I32, [P, I32, PI32, PI32, I32]),
             "orc_p2p_read_cells": (I32, [P, P, P, P]),
             "orc_p2p_read_live": (I32, [P, P, P]),
@@ -187,6 +188,13 @@ class OracleP2P:
     def add_local_input(self, handle: int, inputs) -> int:
         a = np.ascontiguousarray(np.broadcast_to(np.asarray(inputs), (self.S,)), dtype=self.input_dtype)
         return self._lib.orc_p2p_add_local_input(self._h, handle, _ptr(a))
+
+    def disconnect_player(self, handle: int, sessions=None) -> int:
+        """P2PSession::disconnect_player(handle) (p2p_session.rs:430-456) in the
+        sessions whose `sessions` entry is true (None: all); first error kind or 0."""
+        m = None if sessions is None else np.ascontiguousarray(np.broadcast_to(np.asarray(sessions), (self.S,)),
+                                                                dtype=np.uint8)
+        return self._lib.orc_p2p_disconnect(self._h, handle, None if m is None else _ptr(m))
 
     def advance(self):
         """(status [S] (0 Ok, 1 PredictionThreshold, 99 panic), load frame [S], AdvanceFrames [S], saves [S])."""

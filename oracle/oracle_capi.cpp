@@ -199,6 +199,7 @@ struct P2PBatchBase {
   virtual ~P2PBatchBase() = default;
   virtual int32_t deliver(int32_t handle, const int32_t* upto, const uint8_t* by_frame, int32_t n_frames) = 0;
   virtual int32_t add_local_input(int32_t handle, const uint8_t* inputs) = 0;
+  virtual int32_t disconnect(int32_t handle, const uint8_t* mask) = 0;
   virtual int32_t advance(int32_t* status, int32_t* load_frame, int32_t* n_adv, int32_t* n_save) = 0;
   virtual int32_t trace(int32_t session, int32_t* kinds, int32_t* frames, int32_t cap) = 0;
   virtual int32_t read_cells(int32_t* cell_frames, uint8_t* images, uint64_t* cs) = 0;
@@ -256,6 +257,18 @@ struct P2PBatch : P2PBatchBase {
       I v{};
       std::memcpy(&v, in + s * sizeof(I), sizeof(I));
       Error e = sess[s]->add_local_input(static_cast<PlayerHandle>(handle), v);
+      if (e.is_err() && first == 0) first = static_cast<int32_t>(e.kind);
+    }
+    return first;
+  }
+
+  // disconnect_player(handle) in every session whose mask byte is set (NULL: all);
+  // returns the first error kind (0 = ok)
+  int32_t disconnect(int32_t handle, const uint8_t* mask) override {
+    int32_t first = 0;
+    for (size_t s = 0; s < sess.size(); ++s) {
+      if (mask && !mask[s]) continue;
+      Error e = sess[s]->disconnect_player(static_cast<PlayerHandle>(handle));
       if (e.is_err() && first == 0) first = static_cast<int32_t>(e.kind);
     }
     return first;
@@ -438,6 +451,9 @@ int32_t orc_p2p_deliver(void* b, int32_t handle, const int32_t* upto, const uint
 }
 int32_t orc_p2p_add_local_input(void* b, int32_t handle, const uint8_t* inputs) {
   return static_cast<P2PBatchBase*>(b)->add_local_input(handle, inputs);
+}
+int32_t orc_p2p_disconnect(void* b, int32_t handle, const uint8_t* mask) {
+  return static_cast<P2PBatchBase*>(b)->disconnect(handle, mask);
 }
 int32_t orc_p2p_advance(void* b, int32_t* status, int32_t* load_frame, int32_t* n_adv, int32_t* n_save) {
   return static_cast<P2PBatchBase*>(b)->advance(status, load_frame, n_adv, n_save);

@@ -13,17 +13,21 @@ import numpy as np
 import pytest
 
 import ggrs_amd as G
+from ggrs_amd._lib import RB_PANIC
 from ggrs_amd.p2p import PlayerType, synth_network
 from oracle import oracle as O
 
 ORC_GAME = {G.Game.EX_GAME: O.EX_GAME, G.Game.STUB: O.STUB, G.Game.BRAWLER: O.BRAWLER}
 
 
-def drive_oracle(orc, local_mask, inputs, upto, remote_in, T, t0=0):
-    """Ticks [t0, T) of the oracle batch; returns per-tick (status, load, nadv, nsave)."""
+def drive_oracle(orc, local_mask, inputs, upto, remote_in, T, t0=0, disc=None):
+    """Ticks [t0, T) of the oracle batch; returns per-tick (status, load, nadv, nsave).
+    disc: {tick: [(handle, session mask)]} disconnect_player calls before that tick."""
     out = []
     P = inputs.shape[1]
     for t in range(t0, T):
+        for h, m in (disc or {}).get(t, []):
+            assert orc.disconnect_player(h, m) == 0
         for h in range(P):
             if not (local_mask >> h) & 1:
                 assert orc.deliver(h, upto[t, h], remote_in[:, h, :]) == 0, orc.last_panic()
@@ -115,6 +119,60 @@ def test_oracle_prediction_threshold_drops_the_requests():
     assert (cur < T).all()
 
 
+INVALID_REQUEST = 2  # ggrs_oracle.hpp ErrorKind::InvalidRequest
+
+
+def test_oracle_disconnect_player_errors_like_reference_test():
+    # tests/test_p2p_session.rs:45-63 (the spectator handle is not part of the batch)
+    orc = O.OracleP2P(O.STUB, 2, 8, 0, 0b01, 3)
+    assert orc.disconnect_player(5) == INVALID_REQUEST  # invalid handle
+    assert orc.disconnect_player(0) == INVALID_REQUEST  # local players cannot be disconnected
+    assert orc.disconnect_player(1) == 0
+    assert orc.disconnect_player(1) == INVALID_REQUEST  # already disconnected
+
+
+def disconnect_schedule(upto, t0, h):
+    """The last frame each session had received from handle h when it is
+    disconnected before tick t0, and a delivery schedule that hands exactly
+    those frames over before the first tick."""
+    last = upto[t0 - 1, h].copy() if t0 > 0 else np.full(upto.shape[2], -1, np.int32)
+    full = upto.copy()
+    full[:, h, :] = last[None, :]
+    return last, full
+
+
+@pytest.mark.parametrize("game", [G.Game.STUB, G.Game.EX_GAME])
+@pytest.mark.parametrize("sparse", [False, True])
+def test_oracle_disconnect_resimulates_to_the_disconnected_truth(game, sparse):
+    # After disconnect_player(h) every frame past h's last input is advanced with
+    # (zeroed, Disconnected), including the frames already simulated on a
+    # prediction (disconnect_frame = last_frame + 1, p2p_session.rs:576-580).
+    # So the late-delivery run must end with the same cells and state as a run
+    # in which h's inputs up to its last frame all arrived before tick 0.
+    S, P, W, T, mask, h, t0 = 24, 3, 8, 90, 0b001, 2, 40
+    dt = np.uint32 if game == G.Game.STUB else np.uint8
+    inputs, upto, rin = synth_network(S, P, T, mask, remote_delay=1, min_lag=1, max_lag=5, dtype=dt,
+                                      mask=0x3 if game == G.Game.STUB else 0x0F)
+    last, full_h = disconnect_schedule(upto, t0, h)
+    lag = O.OracleP2P(ORC_GAME[game], P, W, 1, mask, S, sparse_saving=sparse, remote_delay=1)
+    res = drive_oracle(lag, mask, inputs, upto, rin, T, disc={t0: [(h, None)]})
+    assert all((r[0] == 0).all() for r in res)
+    loads = np.array([r[1] for r in res])
+    assert (loads[t0] != G.NULL_FRAME).any(), "the disconnect must roll sessions back"
+    # the truth run still receives the other remote (handle 1) late: compare only
+    # after both runs have confirmed everything they saved
+    truth = O.OracleP2P(ORC_GAME[game], P, W, 1, mask, S, sparse_saving=sparse, remote_delay=1)
+    drive_oracle(truth, mask, inputs, full_h, rin, T, disc={t0: [(h, None)]})
+    np.testing.assert_array_equal(lag.read_live()[0], truth.read_live()[0])
+    a, b = lag.read_cells(), truth.read_cells()
+    if not sparse:  # sparse saving picks its cells by the confirmed frame, which depends on delivery timing
+        np.testing.assert_array_equal(a[0], b[0])
+    same = (a[0] == b[0]) & (a[0] >= 0)
+    assert same.sum() >= S
+    for x, y in zip(a[1:], b[1:]):
+        np.testing.assert_array_equal(x[same], y[same])
+
+
 # ---------------------------------------------------------------------------- device vs oracle
 def gpu_pair(game, S, P, W, d, rd, mask, sparse, lane_per_session=False, fanout=False):
     b = (G.SessionBuilder(game, num_sessions=S).with_num_players(P).with_max_prediction_window(W)
@@ -127,18 +185,21 @@ def gpu_pair(game, S, P, W, d, rd, mask, sparse, lane_per_session=False, fanout=
     return sess, orc
 
 
-def compare_state(sess, orc, tick):
+def compare_state(sess, orc, tick, alive=None):
+    """Cells, live state and frames of the device batch == the oracle's
+    (sessions where `alive` is true; a panicked session is dead)."""
     tags, imgs, cs = sess.read_cells()
     otags, oimgs, ocs = orc.read_cells()
-    np.testing.assert_array_equal(tags, otags, err_msg=f"cell frames, tick {tick}")
-    valid = otags >= 0
+    a = np.ones(tags.shape[1], bool) if alive is None else alive
+    np.testing.assert_array_equal(tags[:, a], otags[:, a], err_msg=f"cell frames, tick {tick}")
+    valid = (otags >= 0) & a[None, :]
     np.testing.assert_array_equal(imgs[valid], oimgs[valid], err_msg=f"cell images, tick {tick}")
     np.testing.assert_array_equal(cs[valid], ocs[valid], err_msg=f"cell checksums, tick {tick}")
-    np.testing.assert_array_equal(sess.read_live(), orc.read_live()[0], err_msg=f"live state, tick {tick}")
+    np.testing.assert_array_equal(sess.read_live()[a], orc.read_live()[0][a], err_msg=f"live state, tick {tick}")
     c, k = sess.frames()
     oc, ok = orc.frames()
-    np.testing.assert_array_equal(c, oc)
-    np.testing.assert_array_equal(k, ok)
+    np.testing.assert_array_equal(c[a], oc[a])
+    np.testing.assert_array_equal(k[a], ok[a])
 
 
 CASES = [  # game, P, W, d, rd, local_mask, sparse, lag range
@@ -260,3 +321,68 @@ def test_gpu_speculative_fanout_state_after_many_ticks(gpu_available):
         np.testing.assert_array_equal(x, y)
     ts, tp = spec.totals(), plain.totals()
     assert ts[3] > 0 and ts[2] + ts[3] == tp[2], (ts, tp)  # every rollback is a load or a select
+
+
+DISC_CASES = [  # game, P, W, d, rd, local_mask, sparse, fanout, lag range
+    (G.Game.EX_GAME, 2, 8, 2, 1, 0b01, False, False, (1, 5)),
+    (G.Game.EX_GAME, 3, 7, 0, 2, 0b010, True, False, (0, 4)),
+    (G.Game.EX_GAME, 4, 8, 1, 1, 0b0001, False, True, (1, 5)),
+    (G.Game.STUB, 2, 8, 1, 0, 0b10, False, False, (1, 5)),
+    (G.Game.EX_GAME, 2, 4, 0, 0, 0b01, False, False, (1, 6)),  # PredictionThreshold around the disconnect
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", DISC_CASES, ids=[f"{c[0].name}-P{c[1]}-W{c[2]}-m{c[5]}-sp{int(c[6])}-fo{int(c[7])}"
+                                                  for c in DISC_CASES])
+def test_gpu_p2p_disconnect_matches_oracle_every_tick(gpu_available, case):
+    # disconnect_player between ticks, for half of the sessions at one tick and
+    # the rest later: statuses, request counts, cells and states equal the
+    # oracle's on every tick; the batch raises InvalidRequest like the reference.
+    import torch
+    game, P, W, d, rd, mask, sparse, fanout, (lo, hi) = case
+    S, T = 70, 80
+    dt = np.uint32 if game == G.Game.STUB else np.uint8
+    inputs, upto, rin = synth_network(S, P, T, mask, rd, lo, hi, dtype=dt, mask=0x3 if game == G.Game.STUB else 0x0F)
+    sess, orc = gpu_pair(game, S, P, W, d, rd, mask, sparse, fanout=fanout)
+    remotes = [h for h in range(P) if not (mask >> h) & 1]
+    local = [h for h in range(P) if (mask >> h) & 1][0]
+    h = remotes[-1]
+    half = np.arange(S) % 2 == 0
+    disc = {30: [(h, half)], 47: [(h, ~half)]}
+    if len(remotes) > 1:
+        disc[55] = [(remotes[0], np.arange(S) % 3 == 0)]
+    di, du, dr = (torch.from_numpy(a).cuda() for a in (inputs, upto, rin))
+    saw_rollback_at_disconnect = False
+    # A disconnect whose last frame is current_frame - 1 sets disconnect_frame =
+    # current_frame, and the reference's load_frame asserts (sync_layer.rs:141-145);
+    # so does loading a cell whose SaveGameState was dropped with a
+    # PredictionThreshold error (:148).  Both implementations panic on exactly
+    # those sessions; after that a session is dead and no longer compared.
+    alive = np.ones(S, bool)
+    for t in range(T):
+        for hh, m in disc.get(t, []):
+            sess.disconnect_player(hh, m)
+        ost, olf, ona, ons = drive_oracle(orc, mask, inputs, upto, rin, t + 1, t0=t, disc=disc)[0]
+        sess.run_ticks(di[t:t + 1], du[t:t + 1], dr)
+        st, lf, na, ns = sess.status()
+        st = np.where(st == RB_PANIC, O.KIND_PANIC, st)
+        np.testing.assert_array_equal(st[alive], ost[alive], err_msg=f"status, tick {t}")
+        alive &= ost != O.KIND_PANIC
+        np.testing.assert_array_equal(lf[alive], olf[alive], err_msg=f"LoadGameState frame, tick {t}")
+        np.testing.assert_array_equal(na[alive], ona[alive], err_msg=f"AdvanceFrame count, tick {t}")
+        np.testing.assert_array_equal(ns[alive], ons[alive], err_msg=f"SaveGameState count, tick {t}")
+        if t in disc:
+            saw_rollback_at_disconnect |= bool((lf[alive] != G.NULL_FRAME).any())
+        if t % 10 == 9 or t in disc or t == T - 1:
+            compare_state(sess, orc, t, alive)
+    assert saw_rollback_at_disconnect
+    assert alive.sum() >= S // 4
+    if W >= 8:
+        assert alive.all() and sess.counters()[2] == 0
+    with pytest.raises(G.InvalidRequest, match="already disconnected"):
+        sess.disconnect_player(h, half)
+    with pytest.raises(G.InvalidRequest, match="Local Player"):
+        sess.disconnect_player(local)
+    with pytest.raises(G.InvalidRequest, match="Invalid Player Handle"):
+        sess.disconnect_player(P)
