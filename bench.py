@@ -193,6 +193,11 @@ def bench_p2p(args):
             bytes_rank += branch / world * (state + 2 + P) + S * args.steps * state * 17 + selects / world * state
         avg_kernel_s = kernel_ms / 1e3 / max(1, launches)
         achieved = bytes_rank / max(1, launches) / avg_kernel_s / 1e9
+        traffic = None  # HBM bytes per launch from the committed PMC profile of this exact configuration
+        if not (args.fanout or args.wire or args.sparse_saving):
+            per_tick = pmc_traffic(f"p2p ex_game P={P} W={W} d={args.input_delay} rd={args.remote_delay} "
+                                   f"lag={lo},{hi} S={S}")
+            traffic = per_tick * args.steps / max(1, launches) if per_tick else None
         line = {
             "metric": "P2P session-frames simulated/sec (node), rollback to the first mispredicted frame",
             "value": adv / elapsed, "unit": "session-frames/s", "n_gpus": world, "steps": args.steps,
@@ -215,7 +220,7 @@ def bench_p2p(args):
                        "prediction_threshold_hits": thr, "panics": panics,
                        "parallelism": f"session-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel_avg_us": avg_kernel_s * 1e6,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel_avg_us": avg_kernel_s * 1e6,
                          "ticks_per_launch": args.steps / max(1, launches), "launches_timed": launches,
                          "kernel": f"p2p_kernel<ExGame<{P},true>>" + (" + fanout_kernel (per tick)" if args.fanout
                                                                           else " (fused P2P ticks)")},

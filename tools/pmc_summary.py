@@ -4,7 +4,7 @@ usage: python3 tools/pmc_summary.py <gpurun_out/prof_TAG> <TAG> [config_key] [ti
 
 Writes profiles/<TAG>_kernel_stats.csv (rocprofv3 --stats, verbatim) and
 profiles/<TAG>_pmc.json: per-kernel average counters per launch, and for the
-dominant kernel (steady_kernel) the HBM bytes per launch and per tick:
+dominant kernel (steady_kernel, or p2p_kernel for a P2P bench) the HBM bytes per launch and per tick:
     hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024
 FETCH_SIZE/WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts half the bytes of
 a wide coalesced read (MI355X_MICROARCH.md §HBM), hence the factor 2 on the
@@ -68,9 +68,10 @@ def main():
                 # steady launches of the measured shape: drop the warm-up launch (first)
                 v = vals[1:] if len(vals) > 1 else vals
                 ent[c] = sum(v) / len(v)
-    steady = [k for k in summary["kernels"] if k.startswith("rb::steady_kernel") or "steady_kernel" in k]
+    # the dominant kernel: the fused steady / P2P kernel of the bench line
+    steady = [k for k in summary["kernels"] if "steady_kernel" in k or "p2p_kernel" in k]
     if steady:
-        k = steady[0]
+        k = max(steady, key=lambda n: summary["kernels"][n].get("total_ns", 0.0))
         e = summary["kernels"][k]
         summary["dominant_kernel"] = k
         if "FETCH_SIZE" in e and "WRITE_SIZE" in e:
