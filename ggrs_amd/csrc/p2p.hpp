@@ -199,7 +199,9 @@ __device__ __forceinline__ uint32_t q_input(DevQueue& q, const R& r, int h, unsi
   return q.pred_val;  // Predicted
 }
 
-template <class G>
+// kSpec / kSparse: the fan-out select and sparse saving are compiled in only
+// where the batch uses them (fewer live scalars: no SGPR spills on the plain path)
+template <class G, bool kSpec, bool kSparse>
 __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
   using InRec = typename G::InRec;
   using CS = typename G::CS;
@@ -326,7 +328,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
   };
   // P2PSession::adjust_gamestate (p2p_session.rs:621-673)
   auto adjust = [&](int32_t first_incorrect, int32_t min_confirmed) __attribute__((always_inline)) {
-    const int32_t to_load = p.sparse ? last_saved : first_incorrect;
+    const int32_t to_load = kSparse ? last_saved : first_incorrect;
     const int32_t count = cur - to_load;
     const unsigned slot = static_cast<unsigned>(to_load % W);
     if (to_load < 0 || to_load > first_incorrect || count <= 0 || count > W || p.tag[slot * Spad + s] != to_load) {
@@ -346,7 +348,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
       q[j].last_req = kNullFrame;
     }
     for (int32_t i = 0; i < count; ++i) {
-      if (p.sparse ? cur == min_confirmed : i > 0) save(cur);
+      if (kSparse ? cur == min_confirmed : i > 0) save(cur);
       advance(cur);
       cur += 1;
     }
@@ -422,11 +424,11 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     first_inc = group_min<L>(first_inc);
     if (disc_frame != kNullFrame) first_inc = min(first_inc, disc_frame);  // session-uniform
     if (first_inc != INT32_MAX) {
-      if (!(p.spec_on && exec && try_select(first_inc, confirmed))) adjust(first_inc, confirmed);
+      if (!(kSpec && exec && try_select(first_inc, confirmed))) adjust(first_inc, confirmed);
       disc_frame = kNullFrame;
     }
     if (status == kP2PStatusPanic) return;
-    if (p.sparse) {  // check_last_saved_state (:778-802)
+    if constexpr (kSparse) {  // check_last_saved_state (:778-802)
       if (cur - last_saved >= W) {
         if (confirmed >= cur) save(cur);
         else adjust(last_saved, confirmed);
@@ -434,7 +436,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     } else {
       save(cur);
     }
-    last_conf = p.sparse ? min(confirmed, last_saved) : confirmed;  // set_last_confirmed_frame (sync_layer.rs:220-244)
+    last_conf = kSparse ? min(confirmed, last_saved) : confirmed;  // set_last_confirmed_frame (sync_layer.rs:220-244)
   };
 
   // ---- the per-tick delivery tensors, loaded one tick ahead: at the top of
@@ -515,7 +517,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     // ---- PredictionThreshold (sync_layer.rs:163-167) is decided by bookkeeping
     // alone: without sparse saving from the confirmed frame, with it by a dry run.
     bool threshold;
-    if (!p.sparse) {
+    if constexpr (!kSparse) {
       int32_t confirmed = INT32_MAX;
 #pragma unroll
       for (int j = 0; j < PPL; ++j) confirmed = min(confirmed, conn_of(j));
