@@ -69,6 +69,25 @@ def cpu_baseline(args, P):
                       f"{secs:.2f} s wall, {nerr} errors"}
 
 
+def measured_copy_gbps(dev, nbytes=1 << 30, iters=10):
+    """Device-to-device copy bandwidth (read + write bytes / time) of a 1 GiB
+    buffer: the STREAM-copy ceiling SURVEY.md 8(d) asks to report next to the
+    8 TB/s spec peak.  Runs outside every timed region."""
+    import torch
+    a = torch.empty(nbytes // 4, dtype=torch.int32, device=dev)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        b.copy_(a)
+    e1.record()
+    e1.synchronize()
+    gbps = 2 * nbytes * iters / (e0.elapsed_time(e1) / 1e3) / 1e9
+    del a, b
+    return gbps
+
+
 def pmc_traffic(cfg_key):
     """HBM bytes per steady-state tick (all sessions) from the committed rocprofv3
     PMC summary of this exact configuration (profiles/*pmc*.json, written by
@@ -427,6 +446,7 @@ def main():
                 "launches_timed": launches,
                 "kernel": (f"steady_kernel<Brawler<{P}>,{cd}>" if brawler else f"steady_kernel<ExGame<{P},true>,{cd}>")
                           + " (fused steady-state ticks)",
+                "measured_copy_GBps": measured_copy_gbps(dev),
             },
             "cpu_baseline": None,
         }
