@@ -131,6 +131,26 @@ def test_oracle_disconnect_player_errors_like_reference_test():
     assert orc.disconnect_player(1) == INVALID_REQUEST  # already disconnected
 
 
+def test_oracle_disconnect_at_the_current_frame_asserts_like_reference():
+    # disconnect_player_at_frame sets disconnect_frame = last_frame + 1 whenever
+    # current_frame > last_frame (p2p_session.rs:576-580).  With last_frame =
+    # current_frame - 1 that is the current frame itself, and adjust_gamestate's
+    # load_frame asserts frame_to_load < current_frame (sync_layer.rs:141-145).
+    # One frame older, the session rolls back one frame and goes on.
+    S, P, mask = 2, 2, 0b01
+    orc = O.OracleP2P(O.EX_GAME, P, 8, 0, mask, S)
+    by_frame = np.zeros((16, S), np.uint8)
+    for t in range(4):
+        orc.deliver(1, [t, t - 1], by_frame)  # after tick 3: session 0 holds frame 3, session 1 frame 2
+        orc.add_local_input(0, [1, 1])
+        assert (orc.advance()[0] == 0).all()
+    assert orc.disconnect_player(1) == 0
+    orc.add_local_input(0, [1, 1])
+    st, lf, na, _ = orc.advance()
+    assert st[0] == O.KIND_PANIC
+    assert st[1] == 0 and lf[1] == 3 and na[1] == 2  # load frame 3, resimulate it, advance frame 4
+
+
 def disconnect_schedule(upto, t0, h):
     """The last frame each session had received from handle h when it is
     disconnected before tick t0, and a delivery schedule that hands exactly
@@ -386,3 +406,23 @@ def test_gpu_p2p_disconnect_matches_oracle_every_tick(gpu_available, case):
         sess.disconnect_player(local)
     with pytest.raises(G.InvalidRequest, match="Invalid Player Handle"):
         sess.disconnect_player(P)
+
+
+@pytest.mark.gpu
+def test_gpu_disconnect_at_the_current_frame_asserts_like_reference(gpu_available):
+    # The device side of test_oracle_disconnect_at_the_current_frame_asserts_like_reference.
+    import torch
+    S, P, mask, T = 2, 2, 0b01, 5
+    sess, orc = gpu_pair(G.Game.EX_GAME, S, P, 8, 0, 0, mask, False)
+    inputs = np.ones((T, P, S), np.uint8)
+    upto = np.zeros((T, P, S), np.int32)
+    for t in range(T):
+        upto[t, 1] = [t, t - 1]
+    rin = np.zeros((16, P, S), np.uint8)
+    di, du, dr = (torch.from_numpy(a).cuda() for a in (inputs, upto, rin))
+    sess.run_ticks(di[:4], du[:4], dr)
+    sess.disconnect_player(1)
+    sess.run_ticks(di[4:], du[4:], dr)
+    st, lf, na, _ = sess.status()
+    assert st[0] == RB_PANIC
+    assert st[1] == 0 and lf[1] == 3 and na[1] == 2
