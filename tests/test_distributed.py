@@ -117,3 +117,29 @@ def test_two_rank_gloo_report_allgather_equals_single_process():
         if orc.current_frame() % INTERVAL == 0:
             ref.append(_reports_for(orc, orc.current_frame() - 1).view(np.int64).reshape(-1, shard.REPORT_WORDS))
     np.testing.assert_array_equal(r0, np.stack(ref))
+
+
+def test_p2p_network_shards_are_slices_of_the_global_network():
+    # bench.py --session p2p on N ranks: rank r generates its sessions
+    # [g0, g1) with first_session = g0.  Weak scaling is only honest if those
+    # shards are exactly the columns of the single-process network, and the
+    # oracle's rollback on a shard equals its rollback on the same columns of
+    # the whole batch (sessions never interact).
+    from ggrs_amd.p2p import synth_network
+    S, P, T, mask, world = 48, 2, 40, 0b01, 2
+    full = synth_network(S, P, T, mask, 2, 1, 5)
+    for rank in range(world):
+        g0, g1 = shard.shard_range(rank, world, S)
+        part = synth_network(g1 - g0, P, T, mask, 2, 1, 5, first_session=g0)
+        for a, b in zip(full, part):
+            np.testing.assert_array_equal(a[..., g0:g1], b)
+    whole = O.OracleP2P(O.EX_GAME, P, 8, 2, mask, S, remote_delay=2)
+    half = O.OracleP2P(O.EX_GAME, P, 8, 2, mask, S // 2, remote_delay=2)
+    inputs, upto, rin = full
+    for t in range(T):
+        for orc, cols in ((whole, slice(0, S)), (half, slice(S // 2, S))):
+            orc.deliver(1, upto[t, 1, cols], rin[:, 1, cols])
+            orc.add_local_input(0, inputs[t, 0, cols])
+            st = orc.advance()[0]
+            assert (st == 0).all()
+    np.testing.assert_array_equal(whole.read_live()[0][S // 2:], half.read_live()[0])
