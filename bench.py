@@ -52,9 +52,72 @@ def init_dist(dist, dev):
         dist.init_process_group(backend)
 
 
+def cpu_threads():
+    """Host cores this process may use: the CPU affinity mask, further bounded by
+    a cgroup CPU quota when one is set (cgroup v2 cpu.max).  The north star asks
+    for the reference CPU path "across all host cores of the same box"; on a
+    shared GPU box that is the CPU share this job is given, not os.cpu_count()
+    (reported next to it)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+def cpu_info(threads):
+    return {"cores": threads, "host_cpus": os.cpu_count()}
+
+
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """--gpus N > 1 without an outside launcher: start N rank processes (one per
+    GPU, RANK/LOCAL_RANK/WORLD_SIZE set, rendezvous on 127.0.0.1) before this
+    process touches the GPU; rank 0's stdout (the JSON line) passes through,
+    the other ranks' stdout goes to stderr.  Returns the worst exit code."""
+    import subprocess
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else sys.stderr))
+    rcs = [None] * n
+    try:
+        while any(rc is None for rc in rcs):
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    rcs[i] = p.poll()
+                    if rcs[i] not in (None, 0):  # one rank failed: the others would hang in a collective
+                        for q in procs:
+                            if q.poll() is None:
+                                q.terminate()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return max(abs(rc) for rc in rcs)
+
+
 def cpu_baseline(args, P):
     from oracle import oracle as O
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads = cpu_threads()
     S, warm, ticks = args.cpu_sessions, 16, args.cpu_ticks
     fn = O.bench_brawler if args.game == "brawler" else O.bench_exgame
     if S is None:
@@ -63,10 +126,10 @@ def cpu_baseline(args, P):
         ticks = 256 if args.game == "brawler" else 384
     secs, nerr = fn(P, args.check_distance, args.input_delay, args.max_prediction, S, warm, ticks, threads, args.seed)
     sf = S * ticks * (args.check_distance + 1)
-    return {"value": sf / secs, "unit": "session-frames/s", "cores": threads, "kind": "port",
+    return {"value": sf / secs, "unit": "session-frames/s", **cpu_info(threads), "kind": "port",
             "sample": f"{S} {args.game} sessions x {ticks} steady-state ticks ({sf} session-frames) of the C++ "
-                      f"line-faithful restatement (reference allocation pattern), {threads} host threads, "
-                      f"{secs:.2f} s wall, {nerr} errors"}
+                      f"line-faithful restatement (reference allocation pattern), {threads} host threads "
+                      f"(every core this job may use), {secs:.2f} s wall, {nerr} errors"}
 
 
 def measured_copy_gbps(dev, nbytes=1 << 30, iters=10):
@@ -103,6 +166,81 @@ def pmc_traffic(cfg_key):
         if d.get("config_key") == cfg_key and d.get("hbm_bytes_per_tick"):
             best = d["hbm_bytes_per_tick"]
     return best
+
+
+def rehearsal(args):
+    """CPU rehearsal of the N-rank path: the self-launcher, the 127.0.0.1
+    rendezvous, the report all-gather and the audit compare, with plan-only
+    batches (device = -1: the host bookkeeping of every tick, no device work)
+    and no GPU.  Each report's checksum is a keyed hash of (global session id,
+    frame) — a replica reports what its owner reports, so the compare must
+    find nothing — except that --rehearsal-corrupt makes rank 0's first
+    replica lie once.  Prints one JSON line with value null."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import ggrs_amd as G
+    from ggrs_amd import shard
+    from ggrs_amd.synth import splitmix64
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group(os.environ.get("GGRS_BENCH_BACKEND", "gloo"))
+    P, cd, S = args.num_players, args.check_distance, args.sessions_per_gpu
+    A = min(args.audit_sessions, S) if world > 1 else 0
+    warm = max(args.warmup, cd + 1)
+    T = warm + args.steps
+    lo, hi = shard.shard_range(rank, world, S * world)
+    nlo = shard.shard_range((rank + 1) % world, world, S * world)[0]
+    inputs = G.synth_inputs(hi - lo, P, T, seed=args.seed, first_session=lo)
+    if A:
+        inputs = np.concatenate([inputs, G.synth_inputs(A, P, T, seed=args.seed, first_session=nlo)], 2)
+    inputs = np.ascontiguousarray(inputs)
+    gid = np.concatenate([np.arange(lo, hi), np.arange(nlo, nlo + A)]).astype(np.uint64)
+    sess = (G.SessionBuilder(G.Game.EX_GAME, num_sessions=S + A, device=-1).with_num_players(P)
+            .with_max_prediction_window(args.max_prediction).with_check_distance(cd)
+            .with_input_delay(args.input_delay).start_synctest_session())
+    interval = args.report_interval or 10
+    gathers = mism = audit_bad = 0
+    first_bad = None
+    t = 0
+    t0 = time.perf_counter()
+    while t < T:
+        n = min(T - t, interval - sess.current_frame() % interval)
+        sess.run_ticks(inputs[t:t + n])
+        t += n
+        if world > 1 and sess.current_frame() % interval == 0:
+            f = sess.current_frame() - 1
+            cs = splitmix64((gid << np.uint64(20)) ^ np.uint64(f))
+            if os.environ.get("GGRS_REHEARSAL_CORRUPT") and rank == 0 and A and gathers == 0:
+                cs[S] ^= np.uint64(1)
+            rep = shard.pack_reports(np.stack([cs, np.zeros_like(cs)], 1), f, np.full(S + A, -1, np.int32))
+            g = shard.gather_reports(torch.from_numpy(rep.view(np.int64).reshape(-1, shard.REPORT_WORDS).copy()))
+            mism += int(shard.count_desynced(g, world, S, A))
+            nbad, detail = shard.audit_compare(g, world, S, A)
+            audit_bad += int(nbad)
+            if first_bad is None and int(nbad):
+                first_bad = [int(x) for x in detail[0]]
+            gathers += 1
+    elapsed = time.perf_counter() - t0
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC, "value": None, "unit": "session-frames/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic", "rehearsal": True,
+            "config": {"workload": f"plan-only rehearsal: {S} sessions/rank + {A} audit replicas, no device work",
+                       "sessions_per_gpu": S, "total_sessions": S * world,
+                       "desync_reports": {"ranks": dist.get_world_size() if world > 1 else 1,
+                                          "backend": dist.get_backend() if world > 1 else None,
+                                          "gathers": gathers, "mismatch_rows_seen": mism,
+                                          "audit_sessions_per_rank": A, "audit_compared": A * world * gathers,
+                                          "audit_desynced": audit_bad, "first_desync": first_bad}},
+            "roofline": None, "cpu_baseline": None}), flush=True)
+    sess.close()
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def bench_p2p(args):
@@ -249,11 +387,11 @@ def bench_p2p(args):
             # the reference rollback path (the oracle's P2PSession + ex_game, reference allocation
             # pattern) on the same arrays: same inputs, same delivery schedule, same rollbacks
             from oracle import oracle as O
-            threads = max(1, min(16, os.cpu_count() or 1))
+            threads = cpu_threads()
             secs, cadv, nerr = O.bench_p2p_exgame(P, W, args.input_delay, mask, args.remote_delay, inputs, upto, rin,
                                                   args.warmup, threads)
             line["cpu_baseline"] = {
-                "value": cadv / secs, "unit": "session-frames/s", "cores": threads, "kind": "port",
+                "value": cadv / secs, "unit": "session-frames/s", **cpu_info(threads), "kind": "port",
                 "sample": f"the full workload ({S} sessions x {args.steps} timed ticks, {cadv} AdvanceFrames) through "
                           f"the C++ restatement of P2PSession rollback (no fan-out: the reference has none), "
                           f"{threads} host threads, {secs:.2f} s wall, {nerr} errors"}
@@ -268,7 +406,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=32)
-    ap.add_argument("--sessions-per-gpu", type=int, default=65536)
+    ap.add_argument("--sessions-per-gpu", type=int, default=None,
+                    help="default: 65,536 at --gpus 1 (BASELINE configs[1]), 131,072 at --gpus N > 1 "
+                         "(configs[4]: 1,048,576 sessions over 8 GPUs)")
     ap.add_argument("--num-players", type=int, default=2)
     ap.add_argument("--check-distance", type=int, default=7)
     ap.add_argument("--max-prediction", type=int, default=8)
@@ -296,7 +436,22 @@ def main():
     ap.add_argument("--fanout", action="store_true",
                     help="p2p: speculative fan-out, 16 candidate inputs per session per tick (BASELINE configs[3]; "
                          "use with --num-players 4)")
+    ap.add_argument("--audit-sessions", type=int, default=64,
+                    help="N>1: each rank also simulates this many sessions of the next rank's shard; after every "
+                         "report all-gather the owner's checksums are compared with the replica's (DesyncDetected)")
+    ap.add_argument("--rehearsal", action="store_true",
+                    help="CPU rehearsal of the N-rank path (launcher, rendezvous, report all-gather, audit compare) "
+                         "with plan-only batches (host bookkeeping, no device): GGRS_BENCH_BACKEND=gloo, no GPU, "
+                         "value null")
     args = ap.parse_args()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args.gpus)  # before anything touches the GPU
+    if args.sessions_per_gpu is None:  # configs[1] at N=1; configs[4]'s per-GPU shard (1,048,576 / 8) at N>1
+        args.sessions_per_gpu = 65536 if args.gpus == 1 else 131072
+        if args.rehearsal:
+            args.sessions_per_gpu = 256
+    if args.rehearsal:
+        return rehearsal(args)
     if args.session == "p2p":
         return bench_p2p(args)
 
@@ -320,22 +475,33 @@ def main():
 
     P, cd = args.num_players, args.check_distance
     S = args.sessions_per_gpu
-    T = args.warmup + args.steps
-    # This rank's shard: global sessions [rank*S, (rank+1)*S); inputs keyed by global id.
+    # The first cd+1 ticks are start-up ticks (no rollback yet, sync_test_session.rs:89): they
+    # always run untimed, together with the requested warmup, so the timed region is steady state.
+    warm = max(args.warmup, cd + 1)
+    T = warm + args.steps
+    # This rank's shard: global sessions [rank*S, (rank+1)*S); inputs keyed by global id.  With
+    # N > 1 the batch also holds A audit replicas: the first A sessions of rank (r+1) % N.
     lo, hi = shard.shard_range(rank, world, S * world)
+    A = min(args.audit_sessions, S) if world > 1 else 0
+    nlo = shard.shard_range((rank + 1) % world, world, S * world)[0]
     brawler = args.game == "brawler"
-    inputs = G.synth_inputs(hi - lo, P, T, seed=args.seed, first_session=lo, mask=0xFF if brawler else 0x0F)
-    dinputs = torch.from_numpy(inputs).to(dev)  # [T, P, S] u8, resident in HBM
+    imask = 0xFF if brawler else 0x0F
+    inputs = G.synth_inputs(hi - lo, P, T, seed=args.seed, first_session=lo, mask=imask)
+    if A:
+        inputs = np.concatenate([inputs, G.synth_inputs(A, P, T, seed=args.seed, first_session=nlo, mask=imask)], 2)
+    dinputs = torch.from_numpy(np.ascontiguousarray(inputs)).to(dev)  # [T, P, S + A] u8, resident in HBM
 
     stream = torch.cuda.Stream(device=dev)
     game = G.Game.BRAWLER if brawler else G.Game.EX_GAME
-    sess = (G.SessionBuilder(game, num_sessions=S, device=local).with_num_players(P)
+    sess = (G.SessionBuilder(game, num_sessions=S + A, device=local).with_num_players(P)
             .with_max_prediction_window(args.max_prediction).with_check_distance(cd)
             .with_input_delay(args.input_delay).with_checked_mismatches(False)
             .with_block_size(args.block_size).start_synctest_session())
     sess.set_stream(stream)
-    reports = torch.zeros((S, shard.REPORT_WORDS), dtype=torch.int64, device=dev)  # rb_checksum_report, 24 B
-    desyncs = torch.zeros((), dtype=torch.int64, device=dev)
+    reports = torch.zeros((S + A, shard.REPORT_WORDS), dtype=torch.int64, device=dev)  # rb_checksum_report, 24 B
+    desyncs = torch.zeros((), dtype=torch.int64, device=dev)  # sessions reporting MismatchedChecksum
+    audit_bad = torch.zeros((), dtype=torch.int64, device=dev)  # DesyncDetected: owner vs replica checksums
+    gathers = [0]
 
     def run(t0, t1):
         """Ticks [t0, t1): native multi-tick calls of at most --ticks-per-launch
@@ -357,13 +523,13 @@ def main():
                 f = sess.current_frame() - 1
                 sess.export_checksum_report(f, reports.data_ptr())
                 gathered = shard.gather_reports(reports)  # RCCL all-gather of desync reports
-                desyncs.add_(shard.count_desynced(gathered))  # mismatch_frame != NULL_FRAME
+                desyncs.add_(shard.count_desynced(gathered, world, S, A))  # mismatch_frame != NULL_FRAME
+                audit_bad.add_(shard.audit_compare(gathered, world, S, A)[0])  # checksum of owner != replica
+                gathers[0] += 1
         return steady_launches
 
-    if args.warmup < cd + 1:
-        raise SystemExit(f"--warmup must cover the {cd + 1} start-up ticks so the timed region is steady state")
     with torch.cuda.stream(stream):
-        run(0, args.warmup)
+        run(0, warm)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -371,7 +537,7 @@ def main():
         sess.profile_enable(True)
         sess.profile_take()
         t0 = time.perf_counter()
-        launches = run(args.warmup, T)
+        launches = run(warm, T)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -379,12 +545,14 @@ def main():
         elapsed = time.perf_counter() - t0
         kernel_ms, timed_ticks = sess.profile_take()  # HIP events around every steady_kernel launch
 
-    nfail = int((sess.mismatches() != G.NULL_FRAME).sum())
+    nfail = int((sess.mismatches()[:S] != G.NULL_FRAME).sum())  # owned sessions only
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    bad = torch.tensor([nfail + int(desyncs.item())], dtype=torch.int64, device=dev)
+    bad = torch.tensor([nfail], dtype=torch.int64, device=dev)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         dist.all_reduce(bad, op=dist.ReduceOp.SUM)
+        ranks_seen = dist.get_world_size()
+        backend = dist.get_backend()
     elapsed = float(el.item())
 
     if rank == 0:
@@ -398,7 +566,7 @@ def main():
         # word implicit); brawler 256 entities x 8 i32
         nw = 256 * 8 if brawler else 5 * P
         bpt = algorithmic_bytes_per_session_tick(P, cd, nw=nw, cs_bytes=2, in_bytes=1)
-        bytes_per_launch = bpt * S * ticks_per_launch
+        bytes_per_launch = bpt * (S + A) * ticks_per_launch  # the kernel runs the audit replicas too
         achieved = bytes_per_launch / avg_kernel_s / 1e9
         cfg_key = f"{args.game} P={P} cd={cd} W={args.max_prediction} d={args.input_delay} S={S}"
         per_tick = pmc_traffic(cfg_key)
@@ -431,6 +599,11 @@ def main():
                 "parallelism": f"session-sharded x{world}" + (f", RCCL allgather of desync reports every "
                                                               f"{args.report_interval} ticks" if world > 1 else ""),
                 "mismatched_sessions": int(bad.item()),
+                "desync_reports": ({"ranks": ranks_seen, "backend": backend, "gathers": gathers[0],
+                                    "interval_ticks": args.report_interval,
+                                    "mismatch_rows_seen": int(desyncs.item()),
+                                    "audit_sessions_per_rank": A, "audit_compared": A * world * gathers[0],
+                                    "audit_desynced": int(audit_bad.item())} if world > 1 else None),
             },
             "roofline": {
                 "bound": "hbm",

@@ -56,11 +56,50 @@ def gather_reports(local, group=None):
     return out
 
 
-def desynced_sessions(gathered):
+def owned_rows(gathered, world: int = 1, owned: int = 0, audit: int = 0):
+    """The rows of owned sessions, in global session order: every rank's batch is
+    ``owned`` sessions followed by ``audit`` replicas (audit_compare)."""
+    if not audit:
+        return gathered
+    return gathered.view(world, owned + audit, -1)[:, :owned].reshape(world * owned, -1)
+
+
+def desynced_sessions(gathered, world: int = 1, owned: int = 0, audit: int = 0):
     """Global ids of sessions whose report carries a mismatch frame (as a tensor)."""
-    mismatch = gathered[:, 2] >> 32  # high half of the last word = mismatch_frame (little endian)
+    rows = owned_rows(gathered, world, owned, audit)
+    mismatch = rows[:, 2] >> 32  # high half of the last word = mismatch_frame (little endian)
     return (mismatch != NULL_FRAME).nonzero().flatten()
 
 
-def count_desynced(gathered):
-    return ((gathered[:, 2] >> 32) != NULL_FRAME).sum()
+def count_desynced(gathered, world: int = 1, owned: int = 0, audit: int = 0):
+    return ((owned_rows(gathered, world, owned, audit)[:, 2] >> 32) != NULL_FRAME).sum()
+
+
+def audit_compare(gathered, world: int, owned: int, audit: int):
+    """Cross-GPU desync detection over the all-gathered reports.
+
+    Rank r's batch holds its ``owned`` sessions and, after them, ``audit``
+    replicas of the first ``audit`` sessions of rank (r+1) % world: the same
+    session simulated independently on two GPUs, like the two peers of a P2P
+    session.  Their ChecksumReports must agree; where they do not, that is the
+    reference's DesyncDetected{frame, local_checksum, remote_checksum}
+    (compare_local_checksums_against_peers, p2p_session.rs:873-898), with the
+    owner as "local".  Returns (count, [k, 4] int64 tensor of (global session
+    id, frame, owner checksum lo, replica checksum lo)) — the count as a tensor,
+    so the call does not synchronise."""
+    import torch
+    if world < 2 or audit <= 0:
+        z = torch.zeros((), dtype=torch.int64, device=gathered.device)
+        return z, torch.zeros((0, 4), dtype=torch.int64, device=gathered.device)
+    rows = gathered.view(world, owned + audit, -1)
+    replica = rows[:, owned:owned + audit]  # rank r's replicas of rank r+1's first sessions
+    owner = torch.roll(rows[:, :audit], shifts=-1, dims=0)  # row r = rank r+1's own reports
+    frame = lambda x: x[..., 2] & 0xFFFFFFFF
+    bad = (replica[..., 0] != owner[..., 0]) | (replica[..., 1] != owner[..., 1]) | (frame(replica) != frame(owner))
+    idx = bad.nonzero()
+    sid = ((idx[:, 0] + 1) % world) * owned + idx[:, 1]
+    own = owner[idx[:, 0], idx[:, 1]]
+    rep = replica[idx[:, 0], idx[:, 1]]
+    detail = torch.stack([sid, frame(own), own[:, 0], rep[:, 0]], 1) if idx.numel() else \
+        torch.zeros((0, 4), dtype=torch.int64, device=gathered.device)
+    return bad.sum(), detail

@@ -143,3 +143,64 @@ def test_p2p_network_shards_are_slices_of_the_global_network():
             st = orc.advance()[0]
             assert (st == 0).all()
     np.testing.assert_array_equal(whole.read_live()[0][S // 2:], half.read_live()[0])
+
+
+def test_audit_compare_finds_exactly_the_corrupted_replica():
+    # rank r's batch = `owned` sessions + `audit` replicas of rank (r+1)'s first sessions
+    world, owned, audit = 3, 5, 2
+    gid = np.concatenate([np.concatenate([np.arange(r * owned, (r + 1) * owned),
+                                          np.arange(((r + 1) % world) * owned, ((r + 1) % world) * owned + audit)])
+                          for r in range(world)]).astype(np.uint64)
+    cs = gid * np.uint64(1000003) + np.uint64(7)
+    rep = shard.pack_reports(np.stack([cs, cs ^ np.uint64(5)], 1), 41, np.full(gid.size, -1, np.int32))
+    g = torch.from_numpy(rep.view(np.int64).reshape(-1, shard.REPORT_WORDS).copy())
+    n, detail = shard.audit_compare(g, world, owned, audit)
+    assert int(n) == 0 and detail.shape == (0, 4)
+    # rank 2's replica of rank 0's session 1 (global 1) disagrees with its owner
+    g2 = g.clone()
+    g2[2 * (owned + audit) + owned + 1, 1] ^= 1  # high checksum word
+    n, detail = shard.audit_compare(g2, world, owned, audit)
+    assert int(n) == 1
+    assert detail.tolist() == [[1, 41, int(g[1, 0]), int(g[1, 0])]]
+    # owned-row helpers skip the replicas
+    assert shard.owned_rows(g, world, owned, audit).shape == (world * owned, shard.REPORT_WORDS)
+    g3 = g.clone()
+    g3[owned, 2] = (g3[owned, 2] & 0xFFFFFFFF) | (7 << 32)  # a replica row carrying a mismatch flag: not owned
+    assert int(shard.count_desynced(g3, world, owned, audit)) == 0
+    g3[owned - 1, 2] = (g3[owned - 1, 2] & 0xFFFFFFFF) | (7 << 32)
+    assert shard.desynced_sessions(g3, world, owned, audit).tolist() == [owned - 1]
+
+
+def _bench_rehearsal(n, corrupt):
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, GGRS_BENCH_BACKEND="gloo")
+    env.pop("WORLD_SIZE", None)
+    if corrupt:
+        env["GGRS_REHEARSAL_CORRUPT"] = "1"
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(n), "--rehearsal", "--steps",
+                        "20", "--warmup", "5", "--report-interval", "10"], env=env, cwd=root, capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_self_launches_ranks_from_a_bare_shell():
+    # bench.py --gpus 2 with no outside launcher: the parent starts the rank
+    # processes (gloo here, RCCL on the GPU box), rank 0 prints one line
+    d = _bench_rehearsal(2, corrupt=False)
+    rep = d["config"]["desync_reports"]
+    assert d["n_gpus"] == 2 and rep["ranks"] == 2 and rep["backend"] == "gloo"
+    # 28 ticks (warmup raised to the 8 start-up ticks + 20 timed), a report every 10 frames
+    assert rep["gathers"] == 2 and rep["audit_compared"] == 2 * 2 * 64 and rep["audit_desynced"] == 0
+
+
+def test_bench_rehearsal_audit_reports_an_injected_desync():
+    d = _bench_rehearsal(3, corrupt=True)
+    rep = d["config"]["desync_reports"]
+    assert rep["ranks"] == 3 and rep["audit_desynced"] == 1
+    assert rep["first_desync"][:2] == [256, 9]  # rank 0's replica of global session 256 (rank 1's first), frame 9

@@ -317,6 +317,61 @@ def test_bench_config_65536_sessions_sampled_parity(gpu_available):
         np.testing.assert_array_equal(gc[sample], ocs[w])
 
 
+def test_config5_shard_131072_sessions_with_audit_replicas(gpu_available):
+    """BASELINE config 5's per-GPU shard as bench.py --gpus 8 runs it on rank 7:
+    global sessions [7*131072, 8*131072) plus 64 audit replicas of rank 0's
+    first sessions, through the fused rb_run_ticks path (58 ticks: 8 start-up
+    + one 50-tick launch).  Full size: no mismatch anywhere.  Sampled owned
+    sessions and every replica are bit-exact with the oracle, and the
+    replicas' checksum reports equal those of the owner's batch (rank 0's
+    shard, run separately): the audit compare of bench.py finds nothing."""
+    import torch
+    from ggrs_amd import shard
+    S, A, P, T, rank = 131072, 64, 2, 58, 7
+    lo = rank * S
+    inputs = np.concatenate([synth_inputs(S, P, T, first_session=lo), synth_inputs(A, P, T, first_session=0)], 2)
+    dev = torch.from_numpy(np.ascontiguousarray(inputs)).cuda()
+    sess = (G.SessionBuilder(G.Game.EX_GAME, num_sessions=S + A).with_num_players(P).with_check_distance(7)
+            .with_input_delay(2).with_checked_mismatches(False).start_synctest_session())
+    assert sess.run_ticks(dev[:8]) == 8 and sess.run_ticks(dev[8:]) == T - 8
+    assert (sess.mismatches() == -1).all()
+    rng = np.random.default_rng(5)
+    sample = np.concatenate([np.sort(rng.choice(S, 64, replace=False)), np.arange(S, S + A)])
+    orc = O.OracleBatch(O.EX_GAME, P, 8, 7, 2, sample.size)
+    for t in range(T):
+        for h in range(P):
+            orc.add_local_input(h, inputs[t, h, sample])
+        k, _ = orc.advance()
+        assert (k == 0).all()
+    gimg, gdcs, _ = sess.read_live()
+    oimg, odcs, _ = orc.read_live()
+    np.testing.assert_array_equal(gimg[sample], oimg)
+    np.testing.assert_array_equal(gdcs[sample], odcs)
+    frames, oc, _, ocs = orc.read_cells()
+    for w, fr in enumerate(frames):
+        gi, gc = sess.read_cell(int(fr))
+        np.testing.assert_array_equal(gi[sample], oc[w])
+        np.testing.assert_array_equal(gc[sample], ocs[w])
+    # the owner of the replicated sessions: rank 0's first A sessions in a batch of their own
+    owner = (G.SessionBuilder(G.Game.EX_GAME, num_sessions=A).with_num_players(P).with_check_distance(7)
+             .with_input_delay(2).with_checked_mismatches(False).start_synctest_session())
+    owner.run_ticks(torch.from_numpy(np.ascontiguousarray(inputs[:, :, S:])).cuda())
+    f = T - 1
+    rep = torch.zeros((S + A, shard.REPORT_WORDS), dtype=torch.int64, device="cuda")
+    own = torch.zeros((A, shard.REPORT_WORDS), dtype=torch.int64, device="cuda")
+    sess.export_checksum_report(f, rep.data_ptr())
+    owner.export_checksum_report(f, own.data_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(rep[S:], own)
+    # a 2-rank gather image: this batch as rank 1 of 2, the owner's batch as rank 0's first sessions
+    # (rank 0's own replicas of rank 1's first sessions are those sessions' rows themselves)
+    g = torch.cat([own, torch.zeros((S - A, shard.REPORT_WORDS), dtype=torch.int64, device="cuda"), rep[:A], rep])
+    n, _ = shard.audit_compare(g, 2, S, A)
+    assert int(n) == 0
+    sess.close()
+    owner.close()
+
+
 # ---------------------------------------------------------------------------- fused steady-state ticks (rb_run_ticks)
 @pytest.mark.parametrize("game,P,W,cd,d", [(G.Game.EX_GAME, 2, 8, 7, 2), (G.Game.EX_GAME, 2, 8, 1, 0),
                                            (G.Game.EX_GAME, 1, 8, 4, 0), (G.Game.EX_GAME, 3, 6, 5, 1),

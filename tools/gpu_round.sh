@@ -6,7 +6,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out
 mkdir -p $OUT
-TAG=${TAG:-r01}
+TAG=${TAG:-r02}
 step() {  # step <name> <timeout> <cmd...>
   local name=$1 t=$2; shift 2
   echo "=== $name ($(date +%T))"
@@ -23,6 +23,8 @@ if [ "$MODE" = all ] || [ "$MODE" = test ]; then
   step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" || true
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
+  python3 -c "import os; print('cpu_count', os.cpu_count(), 'affinity', len(os.sched_getaffinity(0)))"; cat /sys/fs/cgroup/cpu.max 2>/dev/null || true
+  step bench_driver 600 python -u bench.py --gpus 1 --steps 20 --warmup 5 || true  # the driver's exact command
   step bench 600 python -u bench.py --steps 400 --warmup 32 || true
 fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
