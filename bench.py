@@ -190,7 +190,7 @@ def rehearsal(args):
         dist.init_process_group(os.environ.get("GGRS_BENCH_BACKEND", "gloo"))
     P, cd, S = args.num_players, args.check_distance, args.sessions_per_gpu
     A = min(args.audit_sessions, S) if world > 1 else 0
-    warm = max(args.warmup, cd + 1)
+    warm = cd + 1 + args.warmup
     T = warm + args.steps
     lo, hi = shard.shard_range(rank, world, S * world)
     nlo = shard.shard_range((rank + 1) % world, world, S * world)[0]
@@ -476,8 +476,9 @@ def main():
     P, cd = args.num_players, args.check_distance
     S = args.sessions_per_gpu
     # The first cd+1 ticks are start-up ticks (no rollback yet, sync_test_session.rs:89): they
-    # always run untimed, together with the requested warmup, so the timed region is steady state.
-    warm = max(args.warmup, cd + 1)
+    # always run untimed, before the W requested warmup ticks, so the timed region is steady state
+    # and the warmup has run the fused steady kernel at least once.
+    warm = cd + 1 + args.warmup
     T = warm + args.steps
     # This rank's shard: global sessions [rank*S, (rank+1)*S); inputs keyed by global id.  With
     # N > 1 the batch also holds A audit replicas: the first A sessions of rank (r+1) % N.

@@ -542,6 +542,22 @@ rb_status rb_run_ticks(rb_batch* b, int32_t n_ticks, const void* inputs, int64_t
     run_start = -1;
     return st;
   };
+  // Early launch.  Once past the start-up ticks (current frame > check
+  // distance) every SyncTest tick has the steady shape: run_ticks supplies
+  // every handle's input, PredictionThreshold cannot trigger (frames ahead =
+  // check distance < max prediction) and nothing else in the bookkeeping
+  // depends on values.  So the fused launch of all n ticks goes to the GPU
+  // first and the host bookkeeping of those ticks runs while it executes;
+  // each tick's lowered program is still checked against the steady shape.
+  const int32_t cur0 = b->plan->current;
+  const bool early = can_fuse && cur0 > b->cfg.check_distance;
+  if (early) {
+    rb_status st = launch_steady_run(b, dev_in, stride, cur0, n_ticks, b->tick);
+    if (st != RB_OK) {
+      if (tmp) (void)hipFreeAsync(tmp, b->stream);
+      return st;
+    }
+  }
   int32_t done = 0;
   for (; done < n_ticks; ++done) {
     for (int h = 0; h < b->P; ++h) b->plan->add_local_input(h);
@@ -560,7 +576,12 @@ rb_status rb_run_ticks(rb_batch* b, int32_t n_ticks, const void* inputs, int64_t
       result = rc == 2 ? fail(b, RB_INVALID_REQUEST, info) : fail(b, RB_PREDICTION_THRESHOLD, "Prediction threshold is reached, cannot proceed without catching up.");
       break;
     }
-    if (can_fuse && is_steady_shape(b, tp)) {
+    if (early) {
+      if (!is_steady_shape(b, tp) || tp.f0 + b->cfg.check_distance != cur0 + done) {
+        result = fail(b, RB_PANIC, "internal: a tick after the start-up ticks did not have the steady shape");
+        break;
+      }
+    } else if (can_fuse && is_steady_shape(b, tp)) {
       if (run_start < 0) {
         run_start = done;
         run_c0 = tp.f0 + b->cfg.check_distance;

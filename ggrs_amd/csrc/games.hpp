@@ -200,6 +200,73 @@ struct ExGame {
       advance_player<kInRange>(&w[5 * j], input, unexpected);
     }
   }
+
+  // ---- phase-split AdvanceFrames for the fused steady ticks (kernels.hpp
+  // steady_kernel).  In State::advance (:259-321) the rotation and its
+  // sine/cosine depend on nothing but the rotation and the inputs, never on
+  // position or velocity.  So `prepare` runs the rotation chain of all N
+  // AdvanceFrames of a tick first — N independent double-precision sincos
+  // evaluations the scheduler can interleave — and `advance_prepared` then
+  // runs each frame's velocity/position chain on the precomputed thrust.
+  // Every f32 operation is the same one on the same operands as in
+  // advance_player, so the results are bit-identical:
+  //   up ? v + t : v - t          ==  v + (up ? t : -t)    (IEEE a - b = a + (-b))
+  //   left ? rot - r : rot + r    ==  rot + (left ? -r : r)
+  static constexpr bool kHasPrep = true;
+  template <int N>
+  struct Prep {
+    float tx[kPlayersPerLane][N], ty[kPlayersPerLane][N];  // signed thrust of frame k
+    float rot[kPlayersPerLane][N + 1];                       // rotation before frame k (rot[N]: after the last)
+    uint32_t thrust[kPlayersPerLane];                        // bit k: UP xor DOWN at frame k
+  };
+  template <bool kInRange, int N, class InRecT>
+  __device__ static void prepare(const uint32_t (&w)[NWL], const InRecT (&in)[N], int lane, Prep<N>& pr,
+                                 uint32_t* unexpected) {
+#pragma unroll
+    for (int j = 0; j < kPlayersPerLane; ++j) {
+      const int i = kSplit ? lane : j;
+      float rot = __uint_as_float(w[5 * j + 4]);
+      pr.thrust[j] = 0u;
+#pragma unroll
+      for (int k = 0; k < N; ++k) {
+        const uint32_t input = player_input(static_cast<InRec>(in[k]), i);
+        const bool up = input & 1u, down = input & 2u, left = input & 4u, right = input & 8u;
+        pr.rot[j][k] = rot;
+        const SinCos sc = sincosf_glibc<kInRange>(rot, unexpected);
+        const float tx = kMovementSpeed * sc.c, ty = kMovementSpeed * sc.s;
+        pr.tx[j][k] = up ? tx : -tx;
+        pr.ty[j][k] = up ? ty : -ty;
+        pr.thrust[j] |= (up != down ? 1u : 0u) << k;
+        const float r1 = rem_euclid<kInRange>(rot + (left ? -kRotationSpeed : kRotationSpeed), 2.0f * kPi);
+        rot = left != right ? r1 : rot;
+      }
+      pr.rot[j][N] = rot;
+    }
+  }
+  // AdvanceFrame k of the prepared tick: friction, thrust, speed clamp, position.
+  template <int N>
+  __device__ static void advance_prepared(uint32_t (&w)[NWL], const Prep<N>& pr, int k) {
+#pragma unroll
+    for (int j = 0; j < kPlayersPerLane; ++j) {
+      uint32_t* p = &w[5 * j];
+      const float old_x = __uint_as_float(p[0]), old_y = __uint_as_float(p[1]);
+      float vx = __uint_as_float(p[2]) * kFriction;
+      float vy = __uint_as_float(p[3]) * kFriction;
+      const bool th = (pr.thrust[j] >> k) & 1u;
+      const float vx1 = vx + pr.tx[j][k], vy1 = vy + pr.ty[j][k];
+      vx = th ? vx1 : vx;
+      vy = th ? vy1 : vy;
+      speed_clamp(vx, vy);
+      float x = old_x + vx, y = old_y + vy;
+      x = fminf(fmaxf(x, 0.0f), kWidth);
+      y = fminf(fmaxf(y, 0.0f), kHeight);
+      p[0] = __float_as_uint(x);
+      p[1] = __float_as_uint(y);
+      p[2] = __float_as_uint(vx);
+      p[3] = __float_as_uint(vy);
+      p[4] = __float_as_uint(pr.rot[j][k + 1]);
+    }
+  }
   // Rotations stay in [0, 2pi] once there (rem_euclid), so a state whose every
   // |rot| < 12 keeps sincos below 120 and rem_euclid's argument below 4pi for
   // any number of AdvanceFrames: no out-of-line library paths needed.
@@ -313,6 +380,7 @@ struct Brawler {
   // State::advance (oracle brawler::State::advance): players, then AI against
   // the players' new positions, then the damage the players took.
   static constexpr bool kHasRangePath = false;
+  static constexpr bool kHasPrep = false;  // plain advance in the fused steady ticks
   __device__ static bool in_range(const uint32_t (&)[NWL]) { return false; }
   template <bool = false>
   __device__ static void advance(uint32_t (&w)[NWL], InRec rec, int lane, uint32_t disc, uint32_t*) {
@@ -440,6 +508,7 @@ struct StubGame {
   __device__ static uint32_t player_input(InRec rec, int p) { return static_cast<uint32_t>(rec >> (32 * p)); }
   // stubs.rs:115-125
   static constexpr bool kHasRangePath = false;
+  static constexpr bool kHasPrep = false;  // plain advance in the fused steady ticks
   __device__ static bool in_range(const uint32_t (&)[NWL]) { return false; }
   template <bool = false>
   __device__ static void advance(uint32_t (&w)[NWL], InRec rec, int, uint32_t, uint32_t*) {
@@ -470,6 +539,7 @@ struct StubEnumGame {
   __device__ static uint32_t player_input(InRec rec, int p) { return (static_cast<uint32_t>(rec) >> (8 * p)) & 0xffu; }
   // stubs_enum.rs:206-216
   static constexpr bool kHasRangePath = false;
+  static constexpr bool kHasPrep = false;  // plain advance in the fused steady ticks
   __device__ static bool in_range(const uint32_t (&)[NWL]) { return false; }
   template <bool = false>
   __device__ static void advance(uint32_t (&w)[NWL], InRec rec, int, uint32_t, uint32_t*) {

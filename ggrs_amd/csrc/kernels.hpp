@@ -330,6 +330,18 @@ __device__ __forceinline__ void settle(U128 v) {
 __device__ __forceinline__ void settle(uint16_t v) { settle(static_cast<uint32_t>(v)); }
 __device__ __forceinline__ void settle(uint8_t v) { settle(static_cast<uint32_t>(v)); }
 
+// The game's phase-split state for N AdvanceFrames (games.hpp kHasPrep), or nothing.
+template <class G, int N, bool = G::kHasPrep>
+struct PrepSel {
+  struct type {};
+};
+template <class G, int N>
+struct PrepSel<G, N, true> {
+  using type = typename G::template Prep<N>;
+};
+template <class G, int N>
+using PrepOf = typename PrepSel<G, N>::type;
+
 // kExp: attribution experiments (RunParams::debug knobs, tools/exp_steady.py);
 // instantiated only in builds made with RB_EXPERIMENTS=1, never in the product.
 template <class G, int CD, bool kExp>
@@ -409,6 +421,8 @@ __global__ void __launch_bounds__(256) steady_kernel(const RunParams p) {
   // one tick before it is used, ahead of that tick's stores.
   InRec newin = new_input(0);
   unsigned slot0 = slot_of(f0);  // f0 % W, advanced with f0
+  [[maybe_unused]] CS pc{};  // Game::periodic_checksum, carried through the launch
+  if constexpr (G::kDisplay) pc = reinterpret_cast<const CS*>(p.periodic_cs)[s];
   // Complete the prologue loads before the loop.  The waitcnt pass merges
   // the loop header's state from the preheader and the latch: a load still
   // pending on the preheader path makes it put a conservative vmcnt at the
@@ -421,6 +435,7 @@ __global__ void __launch_bounds__(256) steady_kernel(const RunParams p) {
 #pragma unroll
   for (int k = 0; k + 1 < CD; ++k) settle(fsw[k]);
   settle(newin);
+  if constexpr (G::kDisplay) settle(pc);
   for (int t = 0; t < p.T; ++t) {
     const int c = p.c0 + t;
     const bool more = t + 1 < p.T;
@@ -428,7 +443,7 @@ __global__ void __launch_bounds__(256) steady_kernel(const RunParams p) {
     const InRec newin_next = new_input(more ? t + 1 : t);
     const InRec next_last = input_of_frame(more ? c + 1 : c);  // frame f0+CD+1 of the next tick
     // ---- InputQueue::add_input for every handle: the new inputs at c + delay
-    if (lead) ring[static_cast<unsigned>((c + p.delay) & (kQueueLen - 1)) * Spad + s] = newin;
+    ring[static_cast<unsigned>((c + p.delay) & (kQueueLen - 1)) * Spad + s] = newin;  // same value from every lane
     // ---- the request stream
     const uint32_t nonce = ((p.tick0 + static_cast<uint32_t>(t)) & 0xffffffu) << 8;
     CsCtx ctx{p.seed, s, nonce};
@@ -438,8 +453,15 @@ __global__ void __launch_bounds__(256) steady_kernel(const RunParams p) {
     // The tick's steps, instantiated twice: with the game's out-of-line range
     // checks compiled out when the whole wave's loaded state is in range
     // (G::in_range, decided once per tick), and the general form otherwise.
+    // Checksums are whole-session values present in every lane of the group
+    // (group_sum), so the checksum stores are issued by every lane: the lanes
+    // of a session write the same value to the same address, and no exec-mask
+    // branch splits the tick into separately scheduled blocks.
     auto steps = [&](auto in_range_tag) __attribute__((always_inline)) {
     constexpr bool kInRange = decltype(in_range_tag)::value;
+    [[maybe_unused]] PrepOf<G, CD + 1> prep;
+    if constexpr (G::kHasPrep && !kExp)  // the tick's rotation chain and thrust first (games.hpp)
+      G::template prepare<kInRange, CD + 1>(w, win, lane, prep, &p.counters[1]);
 #pragma unroll
     for (int k = 0; k <= CD; ++k) {
       const int f = f0 + k;
@@ -448,37 +470,44 @@ __global__ void __launch_bounds__(256) steady_kernel(const RunParams p) {
         const CS cval = (dbg & 4u) ? CS{} : G::checksum(w, f, lane, ctx);
         const unsigned slot = slot_after(slot0, k);
         if (!(dbg & 2u)) store_words<NW>(p.snap + slot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), w);
-        if (lead) csa[slot * Spad + s] = cval;
+        csa[slot * Spad + s] = cval;
         if (k == CD) {
-          if (lead) fsa[slot * Spad + s] = cval;  // first save of frame c: first-seen
+          fsa[slot * Spad + s] = cval;  // first save of frame c: first-seen
           recorded = cval;
         } else if (cval != fsw[k - 1]) {
           mismatch = f;  // newest mismatching frame wins
         }
+        // ex_game periodic_checksum (frame % CHECKSUM_PERIOD == 0, ex_game.rs:104-111): the state an
+        // AdvanceFrame reaches at frame f is the one this save checksums, so the value is this one
+        if constexpr (G::kDisplay) pc = (f % 100 == 0) ? cval : pc;
         // Same lane, same address, program order: this load returns the cell just stored.
         if (k == 1 && more)
           load_words<NW>(p.snap + slot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), wn);
       }
       if (dbg & 1u)
         w[0] += win[k];
+      else if constexpr (G::kHasPrep && !kExp)
+        G::advance_prepared(w, prep, k);  // AdvanceFrame{inputs}
       else
         G::template advance<kInRange>(w, (dbg & 32u) ? static_cast<InRec>(win[k] & static_cast<InRec>(dbg >> 8)) : win[k],
                                       lane, 0u, &p.counters[1]);  // AdvanceFrame{inputs}
-      if ((f + 1) % 100 == 0) {  // ex_game periodic_checksum (frame % CHECKSUM_PERIOD == 0)
-        ctx.nonce = nonce + 128u + static_cast<uint32_t>(k);
-        const CS cval = G::checksum(w, f + 1, lane, ctx);
-        if (G::kDisplay && lead) reinterpret_cast<CS*>(p.periodic_cs)[s] = cval;
-      }
     }
     };
     if (G::kHasRangePath && __all(G::in_range(w)))
       steps(std::true_type{});
     else
       steps(std::false_type{});
-    if constexpr (G::kDisplay) {  // Game::last_checksum after the final AdvanceFrame
-      ctx.nonce = nonce + 255u;
-      const CS cval = G::checksum(w, c + 1, lane, ctx);
-      if (lead) reinterpret_cast<CS*>(p.last_cs)[s] = cval;
+    if constexpr (G::kDisplay) {
+      // Game::last_checksum after the final AdvanceFrame (frame c+1) and the periodic checksum
+      // when c+1 is a multiple of 100, as the session leaves the launch: at its last tick, or at
+      // the tick it stops.  The display value of every earlier tick is overwritten unobserved.
+      if (!more || (mismatch != kNullFrame && !dbg)) {
+        ctx.nonce = nonce + 255u;
+        const CS cval = G::checksum(w, c + 1, lane, ctx);
+        reinterpret_cast<CS*>(p.last_cs)[s] = cval;
+        pc = ((c + 1) % 100 == 0) ? cval : pc;
+        reinterpret_cast<CS*>(p.periodic_cs)[s] = pc;
+      }
     }
     if (mismatch != kNullFrame && !dbg) {  // experiments (debug knobs) change results: never freeze
       store_words<NW>(p.live, static_cast<int>(Gpad), static_cast<int>(g), w);

@@ -195,8 +195,8 @@ def test_bench_self_launches_ranks_from_a_bare_shell():
     d = _bench_rehearsal(2, corrupt=False)
     rep = d["config"]["desync_reports"]
     assert d["n_gpus"] == 2 and rep["ranks"] == 2 and rep["backend"] == "gloo"
-    # 28 ticks (warmup raised to the 8 start-up ticks + 20 timed), a report every 10 frames
-    assert rep["gathers"] == 2 and rep["audit_compared"] == 2 * 2 * 64 and rep["audit_desynced"] == 0
+    # 33 ticks (8 start-up + 5 warmup + 20 timed), a report every 10 frames
+    assert rep["gathers"] == 3 and rep["audit_compared"] == 3 * 2 * 64 and rep["audit_desynced"] == 0
 
 
 def test_bench_rehearsal_audit_reports_an_injected_desync():
