@@ -50,7 +50,9 @@ enum : int {
   QF_LAST_REQ = 4,     // InputQueue::last_requested_frame
   QF_CONN_LAST = 5,    // ConnectionStatus::last_frame (messages.rs:5-18)
   QF_DISC = 6,         // ConnectionStatus::disconnected (0 / 1)
-  QF_COUNT = 7,
+  QF_TAIL = 7,         // InputQueue: frame of inputs[tail] (input_queue.rs:83-101)
+  QF_LEN = 8,          // InputQueue::length
+  QF_COUNT = 9,
 };
 constexpr int kQsFields = QS_PLAYER0 + QF_COUNT * 4;
 // trace rows (the last tick of the last launch): LoadGameState frame, AdvanceFrame count, SaveGameState count
@@ -65,6 +67,41 @@ constexpr int kSpecBranches = 16;
 // spec_meta rows: first speculated frame (base), frame the branch states are at
 // (end), speculated handle, valid flag
 enum : int { SM_BASE = 0, SM_END = 1, SM_PLAYER = 2, SM_VALID = 3, SM_COUNT = 4 };
+
+// ---------------------------------------------------------------------------
+// Desync detection (p2p_session.rs:154-157, 313-316, 873-928; the UdpProtocol
+// side: protocol.rs:27, 176-178, 710-742).  Per session, all of it touched
+// only by the session's lead lane and only on ticks where current_frame %
+// interval == 0 (DesyncDetection::On{interval}):
+//   lh   local_checksum_history  HashMap<Frame, u128>: unordered slots, NULL_FRAME = empty
+//   rh   per remote handle, UdpProtocol::checksum_history: a FIFO — on_checksum_report
+//        only inserts frames above last_added_checksum_frame, so insertion order is
+//        frame order and its retain (frame > last_added - 32) pops from the front
+//   ob   the ChecksumReports sent since the last rb_p2p_take_checksum_reports (ring)
+//   ev   GGRSEvent::DesyncDetected{frame, local, remote, addr} (ring of the newest)
+// Both histories hold at most MAX_CHECKSUM_HISTORY_SIZE + 1 = 33 entries at
+// any time (the retain runs once the map has more than 32).
+constexpr int32_t kMaxChecksumHistory = 32;  // protocol.rs:27 MAX_CHECKSUM_HISTORY_SIZE
+constexpr int kCsHist = 34;
+constexpr int kOutbox = 8;   // = RB_P2P_REPORTS_PER_TAKE
+constexpr int kEvents = 16;  // = RB_P2P_EVENTS_KEPT
+struct DesyncParams {
+  int32_t* lh_frame;  // [kCsHist][Spad]
+  uint64_t* lh_cs;    // [kCsHist][Spad]
+  int32_t* rh_frame;  // [4][kCsHist][Spad] FIFO ring per remote handle
+  uint64_t* rh_lo;    // [4][kCsHist][Spad]
+  uint64_t* rh_hi;    // [4][kCsHist][Spad]
+  int32_t* rh_meta;   // [4][3][Spad]: head, length, last_added_checksum_frame
+  int32_t* ob_frame;  // [kOutbox][Spad]
+  uint64_t* ob_cs;    // [kOutbox][Spad]
+  uint32_t* ob_n;     // [Spad] reports sent since the last take
+  uint32_t* ev_n;     // [Spad] DesyncDetected events since create
+  int32_t* ev_frame;  // [kEvents][Spad] ring, slot = event index % kEvents
+  int32_t* ev_handle;
+  uint64_t* ev_local;
+  uint64_t* ev_remote;
+  int32_t interval;   // 0 = DesyncDetection::Off
+};
 
 struct P2PParams {
   uint32_t* snap;
@@ -96,7 +133,84 @@ struct P2PParams {
   int32_t S, Spad, W, delay, remote_delay, T;
   uint32_t local_mask;
   int32_t sparse;
+  DesyncParams ds;
 };
+
+// check_checksum_send_interval + compare_local_checksums_against_peers
+// (p2p_session.rs:873-928) for session s at current frame `cur`, after
+// set_last_confirmed_frame (:306-316).  Lead lane only.  Returns false when the
+// reference would panic ("cell not found!", :907-910).  The compare walks the
+// remote handles in ascending order and each history in frame order (the
+// reference iterates HashMaps; the order of its events is unspecified).
+template <class CS>
+__device__ __noinline__ bool desync_step(const DesyncParams& d, const CS* __restrict__ cs, const int32_t* __restrict__ tag,
+                                         unsigned s, unsigned Spad, int32_t cur, int32_t last_saved, int32_t W,
+                                         int P, uint32_t local_mask) {
+  if (cur % d.interval != 0) return true;  // both steps act on interval frames only
+  auto at = [&](int k) { return static_cast<size_t>(k) * Spad + s; };
+  int32_t lf[kCsHist];
+#pragma unroll
+  for (int k = 0; k < kCsHist; ++k) lf[k] = d.lh_frame[at(k)];
+  const int32_t frame_to_send = last_saved - 1;
+  if (frame_to_send > W) {
+    const unsigned slot = static_cast<unsigned>(frame_to_send % W);
+    if (tag[slot * Spad + s] != frame_to_send) return false;  // saved_state_by_frame(..).unwrap_or_else(panic)
+    const uint64_t c = to_u128(cs[slot * Spad + s]).lo;  // P2P games' checksums are < 2^64
+    const uint32_t n = d.ob_n[s];  // send_checksum_report to every remote endpoint
+    d.ob_frame[at(static_cast<int>(n % kOutbox))] = frame_to_send;
+    d.ob_cs[at(static_cast<int>(n % kOutbox))] = c;
+    d.ob_n[s] = n + 1;
+    int slot_of = -1, empty = -1;  // local_checksum_history.insert(frame_to_send, checksum)
+#pragma unroll
+    for (int k = kCsHist - 1; k >= 0; --k) {
+      slot_of = lf[k] == frame_to_send ? k : slot_of;
+      empty = lf[k] == kNullFrame ? k : empty;
+    }
+    const int k = slot_of >= 0 ? slot_of : empty;
+    if (k < 0) return false;  // cannot happen: at most 33 entries
+    d.lh_frame[at(k)] = frame_to_send;
+    d.lh_cs[at(k)] = c;
+#pragma unroll
+    for (int j = 0; j < kCsHist; ++j) lf[j] = j == k ? frame_to_send : lf[j];
+  }
+  int len = 0;
+#pragma unroll
+  for (int k = 0; k < kCsHist; ++k) len += lf[k] != kNullFrame;
+  if (len > kMaxChecksumHistory) {  // retain(|&frame, _| frame > current - MAX_CHECKSUM_HISTORY_SIZE)
+#pragma unroll
+    for (int k = 0; k < kCsHist; ++k)
+      if (lf[k] != kNullFrame && lf[k] <= cur - kMaxChecksumHistory) {
+        lf[k] = kNullFrame;
+        d.lh_frame[at(k)] = kNullFrame;
+      }
+  }
+  for (int h = 0; h < P; ++h) {  // compare_local_checksums_against_peers
+    if ((local_mask >> h) & 1u) continue;
+    const size_t m = static_cast<size_t>(h) * 3;
+    const int head = d.rh_meta[at(static_cast<int>(m))], n = d.rh_meta[at(static_cast<int>(m + 1))];
+    for (int i = 0; i < n; ++i) {
+      const size_t r = static_cast<size_t>(h) * kCsHist + static_cast<size_t>((head + i) % kCsHist);
+      const int32_t rf = d.rh_frame[at(static_cast<int>(r))];
+      int li = -1;
+#pragma unroll
+      for (int k = 0; k < kCsHist; ++k) li = lf[k] == rf ? k : li;
+      if (li < 0) continue;
+      const uint64_t lc = d.lh_cs[at(li)], rlo = d.rh_lo[at(static_cast<int>(r))];
+      const uint64_t rhi = d.rh_hi[at(static_cast<int>(r))];
+      if (lc != rlo || rhi != 0) {  // local u128 checksums are < 2^64 for every P2P game
+        const uint32_t e = d.ev_n[s];
+        const int q = static_cast<int>(e % kEvents);
+        d.ev_frame[at(q)] = rf;
+        d.ev_handle[at(q)] = h;
+        d.ev_local[at(q)] = lc;
+        d.ev_remote[at(q)] = rlo;
+        d.ev_n[s] = e + 1;
+      }
+    }
+  }
+  return true;
+}
+
 
 // Lane-group reductions over groups of L consecutive lanes (1, 2, 4 or 64).
 template <int L>
@@ -111,13 +225,18 @@ __device__ __forceinline__ int32_t group_min(int32_t v) {
   return v;
 }
 
-// One InputQueue (input_queue.rs) in registers, minus the tail/length
-// bookkeeping, which only feeds asserts on valid runs: a frame is confirmed iff
-// it is <= last_added_frame.  The inputs live in the HBM ring.
+// One InputQueue (input_queue.rs) in registers.  A frame is confirmed iff it is
+// <= last_added_frame; the tail (frame of inputs[tail]) and the length feed the
+// reference's `length <= INPUT_QUEUE_LENGTH` assert (:181), the one a caller
+// of the batch can trip: remote inputs delivered more than 128 frames past the
+// frames the session has discarded would overwrite ring entries still needed.
+// The inputs live in the HBM ring.
 struct DevQueue {
   int32_t last_added, pred_frame, first_inc, last_req, conn_last;
   uint32_t pred_val;
   bool disc;  // ConnectionStatus::disconnected: set between launches only (rb_p2p_disconnect_player)
+  int32_t tail, len;
+  bool overflow;  // the :181 assert fired (the session panics)
 };
 
 template <int IB>
@@ -164,6 +283,9 @@ constexpr size_t p2p_lds_bytes(int block) {
 template <class R>
 __device__ __forceinline__ void q_add_by_frame(DevQueue& q, const R& r, int h, unsigned s, int32_t f, uint32_t v) {
   r.put(f, h, s, v);
+  q.tail = q.len == 0 ? f : q.tail;  // the first entry ever sits at the tail
+  q.len += 1;
+  q.overflow |= q.len > kQueueLen;  // assert!(self.length <= INPUT_QUEUE_LENGTH)
   q.last_added = f;
   if (q.pred_frame != kNullFrame) {
     if (q.first_inc == kNullFrame && v != q.pred_val) q.first_inc = f;
@@ -182,6 +304,17 @@ __device__ __forceinline__ int32_t q_add(DevQueue& q, const R& r, int h, unsigne
   q_add_by_frame(q, r, h, s, f, v);
   return f;
 }
+// input_queue.rs:83-101 discard_confirmed_frames(frame)
+__device__ __forceinline__ void q_discard(DevQueue& q, int32_t frame) {
+  if (q.last_req != kNullFrame) frame = min(frame, q.last_req);
+  if (frame >= q.last_added) {  // delete all but the most recent (only a disconnected remote gets here)
+    q.tail = q.last_added;
+    q.len = 1;
+  } else if (frame > q.tail) {
+    q.len -= frame - q.tail;
+    q.tail = frame;
+  }
+}
 // input_queue.rs:104-146 input(requested_frame)
 template <class R>
 __device__ __forceinline__ uint32_t q_input(DevQueue& q, const R& r, int h, unsigned s, int32_t f) {
@@ -199,9 +332,10 @@ __device__ __forceinline__ uint32_t q_input(DevQueue& q, const R& r, int h, unsi
   return q.pred_val;  // Predicted
 }
 
-// kSpec / kSparse: the fan-out select and sparse saving are compiled in only
-// where the batch uses them (fewer live scalars: no SGPR spills on the plain path)
-template <class G, bool kSpec, bool kSparse>
+// kSpec / kSparse / kDesync: the fan-out select, sparse saving and desync
+// detection are compiled in only where the batch uses them (fewer live
+// scalars: no SGPR spills on the plain path)
+template <class G, bool kSpec, bool kSparse, bool kDesync>
 __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
   using InRec = typename G::InRec;
   using CS = typename G::CS;
@@ -215,6 +349,10 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
   const int lane = static_cast<int>(g % L);
   const bool lead = lane == 0;
   if (s >= static_cast<unsigned>(p.S)) return;  // whole lane groups leave together
+  // A session that hit a reference assert stays stopped (the reference
+  // process would have aborted): it reports RB_PANIC from then on and its
+  // state, cells and queues stay as the panic left them.
+  if (p.status[s] == kP2PStatusPanic) return;
   const unsigned Spad = static_cast<unsigned>(p.Spad), Gpad = Spad * L;
   const unsigned slot_words = static_cast<unsigned>(NW) * Gpad;
   const int W = p.W;
@@ -244,8 +382,11 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
       q[j].last_req = *qrow(QF_LAST_REQ, h);
       q[j].conn_last = *qrow(QF_CONN_LAST, h);
       q[j].disc = *qrow(QF_DISC, h) != 0;
+      q[j].tail = *qrow(QF_TAIL, h);
+      q[j].len = *qrow(QF_LEN, h);
+      q[j].overflow = false;
     } else {  // padding lane of a 4-lane group (P = 3): no player
-      q[j] = DevQueue{kNullFrame, kNullFrame, kNullFrame, kNullFrame, INT32_MAX, 0u, false};
+      q[j] = DevQueue{kNullFrame, kNullFrame, kNullFrame, kNullFrame, INT32_MAX, 0u, false, kNullFrame, 0, false};
     }
   }
   // disconnect_player between launches: P2PSession::disconnect_frame, consumed
@@ -437,6 +578,10 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
       save(cur);
     }
     last_conf = kSparse ? min(confirmed, last_saved) : confirmed;  // set_last_confirmed_frame (sync_layer.rs:220-244)
+    if (last_conf > 0) {
+#pragma unroll
+      for (int j = 0; j < PPL; ++j) q_discard(q[j], last_conf - 1);
+    }
   };
 
   // ---- the per-tick delivery tensors, loaded one tick ahead: at the top of
@@ -468,6 +613,17 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     const uint8_t* src = p.remote_in + (static_cast<size_t>(f) * P + h) * p.S * IB + static_cast<size_t>(s) * IB;
     return IB == 4 ? *reinterpret_cast<const uint32_t*>(src) : *src;
   };
+  // desync detection after set_last_confirmed_frame (p2p_session.rs:313-316):
+  // the lead lane runs it, the group learns whether it panicked
+  auto run_desync = [&]() __attribute__((always_inline)) -> bool {
+    if constexpr (!kDesync) {
+      return true;
+    } else {
+      bool ok = true;
+      if (lead) ok = desync_step<CS>(p.ds, csa, p.tag, s, Spad, cur, last_saved, W, P, p.local_mask);
+      return group_min<L>(ok ? 1 : 0) == 1;
+    }
+  };
   int32_t up[PPL];
   uint32_t lin[PPL], rv[PPL][kPre];
 #pragma unroll
@@ -489,6 +645,8 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
       lin_n[j] = load_local(tn, j);
     }
     status = kP2PStatusOk;
+    load_frame = kNullFrame;
+    nadv = nsave = 0;
     // ---- poll_remote_clients: Event::Input in frame order (handle_event, :838-852)
 #pragma unroll
     for (int j = 0; j < PPL; ++j) {
@@ -513,6 +671,15 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
       const int32_t f = remote_start(j);
 #pragma unroll
       for (int k = 0; k < kPre; ++k) rv_n[j][k] = load_remote(j, f + k);
+    }
+    {  // input_queue.rs:181 assert!(self.length <= INPUT_QUEUE_LENGTH) fired during the poll
+      bool ovf = false;
+#pragma unroll
+      for (int j = 0; j < PPL; ++j) ovf |= q[j].overflow;
+      if (group_min<L>(ovf ? 0 : 1) == 0) {
+        status = kP2PStatusPanic;
+        break;
+      }
     }
     // ---- PredictionThreshold (sync_layer.rs:163-167) is decided by bookkeeping
     // alone: without sparse saving from the confirmed frame, with it by a dry run.
@@ -551,9 +718,17 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
       load_frame = kNullFrame;       // and the user never sees the dropped requests
       nadv = nsave = 0;
       if (lead) atomicAdd(&p.counters[0], 1u);
+      if (!run_desync()) {  // desync detection ran before add_local_input failed (:313-316, :334)
+        status = kP2PStatusPanic;
+        break;
+      }
     } else {
       rollback_and_save();
       if (status == kP2PStatusPanic) break;
+      if (!run_desync()) {
+        status = kP2PStatusPanic;
+        break;
+      }
       // ---- local inputs: SyncLayer::add_local_input (sync_layer.rs:159-174)
 #pragma unroll
       for (int j = 0; j < PPL; ++j) {
@@ -593,6 +768,8 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     *qrow(QF_FIRST_INC, h) = q[j].first_inc;
     *qrow(QF_LAST_REQ, h) = q[j].last_req;
     *qrow(QF_CONN_LAST, h) = q[j].conn_last;
+    *qrow(QF_TAIL, h) = q[j].tail;
+    *qrow(QF_LEN, h) = q[j].len;
   }
   if (lead) {
     p.qs[QS_CUR * Spad + s] = cur;
@@ -625,6 +802,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
 // misprediction into a select (try_select) instead of a resimulation.
 // ---------------------------------------------------------------------------
 struct FanParams {
+  const int32_t* status;  // [Spad] rb_status of the last advance_frame (panicked sessions are skipped)
   const uint32_t* snap;
   const int32_t* tag;
   const void* ring;
@@ -676,7 +854,7 @@ __global__ void __launch_bounds__(256) fanout_kernel(const FanParams p) {
 #pragma unroll
   for (int h = 0; h < P; ++h) any_disc |= qrow(QF_DISC, h) != 0;
   const int32_t base = la_rs + 1;  // first unconfirmed frame of the speculated player
-  const bool valid = !any_disc && rs >= 0 && base < cur && base + W > cur && base >= 0 &&
+  const bool valid = p.status[s] != kP2PStatusPanic && !any_disc && rs >= 0 && base < cur && base + W > cur && base >= 0 &&
                      p.tag[static_cast<unsigned>(base % W) * Spad + s] == base;
   if (k == 0 && lane == 0) {
     p.spec_meta[SM_BASE * Spad + s] = base;

@@ -32,6 +32,7 @@ struct rb_p2p {
   int32_t* spec_meta = nullptr;
   std::vector<uint8_t> disconnected;  // host mirror [P][S] of ConnectionStatus::disconnected (validation)
   uint8_t* disc_mask = nullptr;       // [S] device copy of rb_p2p_disconnect_player's session mask
+  DesyncParams ds{};                  // desync detection buffers (desync_interval > 0)
   bool prof = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev;
   size_t prof_used = 0;
@@ -60,6 +61,11 @@ void free_all(rb_p2p* b) {
                   b->disc_mask};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
+  void* dptrs[] = {b->ds.lh_frame, b->ds.lh_cs,    b->ds.rh_frame, b->ds.rh_lo,     b->ds.rh_hi,
+                   b->ds.rh_meta,  b->ds.ob_frame, b->ds.ob_cs,    b->ds.ob_n,      b->ds.ev_n,
+                   b->ds.ev_frame, b->ds.ev_handle, b->ds.ev_local, b->ds.ev_remote};
+  for (void* q : dptrs)
+    if (q) (void)hipFree(q);
   for (auto& pr : b->prof_ev) {
     (void)hipEventDestroy(pr.first);
     (void)hipEventDestroy(pr.second);
@@ -86,6 +92,58 @@ __global__ void p2p_disconnect_kernel(int32_t* qs, const uint8_t* mask, int32_t 
   const int32_t last = qs[(QS_PLAYER0 + QF_CONN_LAST * 4 + h) * sp + s];
   qs[(QS_PLAYER0 + QF_DISC * 4 + h) * sp + s] = 1;
   if (qs[QS_CUR * sp + s] > last) qs[QS_DISC_FRAME * sp + s] = last + 1;
+}
+
+// UdpProtocol::on_checksum_report (protocol.rs:710-722) for the endpoint of
+// remote handle h in every session: the peer's reports, oldest first,
+// in[k * S + s] for k < K (frame NULL_FRAME = none).
+__global__ void p2p_receive_reports_kernel(DesyncParams d, const rb_checksum_report* __restrict__ in, int K, int S,
+                                           int Spad, int h) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= S) return;
+  auto at = [&](size_t k) { return k * static_cast<size_t>(Spad) + static_cast<size_t>(s); };
+  const size_t m = static_cast<size_t>(h) * 3;
+  int head = d.rh_meta[at(m)], n = d.rh_meta[at(m + 1)], last = d.rh_meta[at(m + 2)];
+  for (int k = 0; k < K; ++k) {
+    const rb_checksum_report r = in[static_cast<size_t>(k) * S + s];
+    if (r.frame == kNullFrame || !(last < r.frame)) continue;
+    if (n > kMaxChecksumHistory) {  // retain(|&frame, _| frame > last_added - MAX): the oldest leave the front
+      while (n > 0 && d.rh_frame[at(static_cast<size_t>(h) * kCsHist + static_cast<size_t>(head))] <= last - kMaxChecksumHistory) {
+        head = (head + 1) % kCsHist;
+        --n;
+      }
+    }
+    last = r.frame;
+    if (n >= kCsHist) continue;  // cannot happen: at most 33 entries
+    const size_t slot = static_cast<size_t>(h) * kCsHist + static_cast<size_t>((head + n) % kCsHist);
+    d.rh_frame[at(slot)] = r.frame;
+    d.rh_lo[at(slot)] = r.checksum_lo;
+    d.rh_hi[at(slot)] = r.checksum_hi;
+    ++n;
+  }
+  d.rh_meta[at(m)] = head;
+  d.rh_meta[at(m + 1)] = n;
+  d.rh_meta[at(m + 2)] = last;
+}
+
+// The reports sent since the last take, oldest first, out[k * S + s] for
+// k < kOutbox (only the newest kOutbox are kept); resets the outbox.
+__global__ void p2p_take_reports_kernel(DesyncParams d, rb_checksum_report* __restrict__ out, int S, int Spad) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= S) return;
+  auto at = [&](int k) { return static_cast<size_t>(k) * static_cast<size_t>(Spad) + static_cast<size_t>(s); };
+  const uint32_t n = d.ob_n[s];
+  const uint32_t cnt = n < static_cast<uint32_t>(kOutbox) ? n : static_cast<uint32_t>(kOutbox);
+  for (int k = 0; k < kOutbox; ++k) {
+    rb_checksum_report r{0, 0, kNullFrame, kNullFrame};
+    if (static_cast<uint32_t>(k) < cnt) {
+      const int q = static_cast<int>((n - cnt + static_cast<uint32_t>(k)) % kOutbox);
+      r.frame = d.ob_frame[at(q)];
+      r.checksum_lo = d.ob_cs[at(q)];
+    }
+    out[static_cast<size_t>(k) * S + s] = r;
+  }
+  d.ob_n[s] = 0;
 }
 
 void image_from_planes(const rb_p2p* b, const std::vector<uint32_t>& planes, int s, int32_t frame, uint8_t* out) {
@@ -121,7 +179,7 @@ rb_status rb_p2p_create(const rb_p2p_config* cfg, rb_p2p** out) {
   if (cfg->max_prediction <= 0)  // builder.rs:136-145
     return pfail(nullptr, RB_INVALID_REQUEST, "Currently, only prediction windows above 0 are supported");
   if (cfg->num_players <= 0 || cfg->num_players > 4 || cfg->num_sessions <= 0 || cfg->input_delay < 0 ||
-      cfg->remote_delay < 0)
+      cfg->remote_delay < 0 || cfg->desync_interval < 0)
     return pfail(nullptr, RB_INVALID_REQUEST, "num_players must be 1..4; sizes and delays non-negative");
   const uint32_t all = (1u << cfg->num_players) - 1u;
   if ((cfg->local_mask & ~all) != 0)  // builder.rs:103-115: handles must be < num_players
@@ -202,11 +260,42 @@ rb_status rb_p2p_create(const rb_p2p_config* cfg, rb_p2p** out) {
     for (int h = 0; h < 4; ++h) {
       qs[(QS_PLAYER0 + QF_PRED_VAL * 4 + h) * Sp + s] = 0;
       qs[(QS_PLAYER0 + QF_DISC * 4 + h) * Sp + s] = 0;  // ConnectionStatus::default: connected
+      qs[(QS_PLAYER0 + QF_LEN * 4 + h) * Sp + s] = 0;   // InputQueue::new: length 0
     }
   }
   b->disconnected.assign(static_cast<size_t>(b->P) * b->S, 0);
   P2P_CREATE(hipMalloc(&b->disc_mask, Sp));
   P2P_CREATE(hipMemcpyAsync(b->qs, qs.data(), qs.size() * 4, hipMemcpyHostToDevice, b->stream));
+  if (cfg->desync_interval > 0) {  // empty histories, outbox and event rings
+    DesyncParams& d = b->ds;
+    d.interval = cfg->desync_interval;
+    const size_t H = kCsHist, R = 4;
+    P2P_CREATE(hipMalloc(&d.lh_frame, H * Sp * 4));
+    P2P_CREATE(hipMalloc(&d.lh_cs, H * Sp * 8));
+    P2P_CREATE(hipMalloc(&d.rh_frame, R * H * Sp * 4));
+    P2P_CREATE(hipMalloc(&d.rh_lo, R * H * Sp * 8));
+    P2P_CREATE(hipMalloc(&d.rh_hi, R * H * Sp * 8));
+    P2P_CREATE(hipMalloc(&d.rh_meta, R * 3 * Sp * 4));
+    P2P_CREATE(hipMalloc(&d.ob_frame, kOutbox * Sp * 4));
+    P2P_CREATE(hipMalloc(&d.ob_cs, kOutbox * Sp * 8));
+    P2P_CREATE(hipMalloc(&d.ob_n, Sp * 4));
+    P2P_CREATE(hipMalloc(&d.ev_n, Sp * 4));
+    P2P_CREATE(hipMalloc(&d.ev_frame, kEvents * Sp * 4));
+    P2P_CREATE(hipMalloc(&d.ev_handle, kEvents * Sp * 4));
+    P2P_CREATE(hipMalloc(&d.ev_local, kEvents * Sp * 8));
+    P2P_CREATE(hipMalloc(&d.ev_remote, kEvents * Sp * 8));
+    P2P_CREATE(hipMemsetAsync(d.lh_frame, 0xff, H * Sp * 4, b->stream));  // NULL_FRAME: empty slot
+    P2P_CREATE(hipMemsetAsync(d.lh_cs, 0, H * Sp * 8, b->stream));
+    P2P_CREATE(hipMemsetAsync(d.rh_frame, 0xff, R * H * Sp * 4, b->stream));
+    std::vector<int32_t> meta(R * 3 * Sp, 0);  // head 0, length 0, last_added_checksum_frame NULL_FRAME
+    for (size_t h = 0; h < R; ++h)
+      for (size_t s = 0; s < Sp; ++s) meta[(h * 3 + 2) * Sp + s] = kNullFrame;
+    P2P_CREATE(hipMemcpy(d.rh_meta, meta.data(), meta.size() * 4, hipMemcpyHostToDevice));
+    P2P_CREATE(hipMemsetAsync(d.ob_n, 0, Sp * 4, b->stream));
+    P2P_CREATE(hipMemsetAsync(d.ev_n, 0, Sp * 4, b->stream));
+    P2P_CREATE(hipMemsetAsync(d.ev_frame, 0xff, kEvents * Sp * 4, b->stream));
+    P2P_CREATE(hipMemsetAsync(d.ev_handle, 0xff, kEvents * Sp * 4, b->stream));
+  }
   // State::new for every session
   std::vector<uint32_t> w0(L * NW), planes(NW * Gp);
   b->ops->init_words(w0.data());
@@ -271,7 +360,9 @@ rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs,
   p.spec_cells = b->spec_cells;
   p.spec_cs = b->spec_cs;
   p.spec_meta = b->spec_meta;
+  p.ds = b->ds;
   FanParams fp{};
+  fp.status = b->status;
   fp.snap = b->snap;
   fp.tag = b->tag;
   fp.ring = b->ring;
@@ -420,6 +511,76 @@ rb_status rb_p2p_totals(rb_p2p* b, uint64_t* out5) {
     uint64_t t = 0;
     for (int s = 0; s < b->S; ++s) t += st[static_cast<size_t>(i) * b->Spad + s];
     out5[i] = t;
+  }
+  return RB_OK;
+}
+
+rb_status rb_p2p_take_checksum_reports(rb_p2p* b, void* dev_out) {
+  if (b->ds.interval <= 0) return pfail(b, RB_INVALID_REQUEST, "desync detection is off (desync_interval = 0)");
+  P2P_TRY(b, hipSetDevice(b->device));
+  hipLaunchKernelGGL(p2p_take_reports_kernel, dim3((b->S + 255) / 256), dim3(256), 0, b->stream, b->ds,
+                     static_cast<rb_checksum_report*>(dev_out), b->S, b->Spad);
+  P2P_TRY(b, hipGetLastError());
+  return RB_OK;
+}
+
+rb_status rb_p2p_receive_checksum_reports(rb_p2p* b, int32_t handle, const void* dev_in, int32_t count) {
+  if (b->ds.interval <= 0) return pfail(b, RB_INVALID_REQUEST, "desync detection is off (desync_interval = 0)");
+  if (handle < 0 || handle >= b->P || ((b->cfg.local_mask >> handle) & 1u))
+    return pfail(b, RB_INVALID_REQUEST, "checksum reports come from a remote handle's endpoint");
+  if (count <= 0) return RB_OK;
+  P2P_TRY(b, hipSetDevice(b->device));
+  hipLaunchKernelGGL(p2p_receive_reports_kernel, dim3((b->S + 255) / 256), dim3(256), 0, b->stream, b->ds,
+                     static_cast<const rb_checksum_report*>(dev_in), count, b->S, b->Spad, handle);
+  P2P_TRY(b, hipGetLastError());
+  return RB_OK;
+}
+
+rb_status rb_p2p_read_desync_events(rb_p2p* b, uint32_t* counts, int32_t* frames, int32_t* handles,
+                                    uint64_t* local_checksums, uint64_t* remote_checksums) {
+  if (b->ds.interval <= 0) return pfail(b, RB_INVALID_REQUEST, "desync detection is off (desync_interval = 0)");
+  const size_t Sp = b->Spad, E = kEvents;
+  std::vector<uint32_t> n;
+  std::vector<int32_t> fr, hd;
+  std::vector<uint64_t> lo, ro;
+  rb_status r = read_rows(b, b->ds.ev_n, 1, n);
+  if (r == RB_OK) r = read_rows(b, b->ds.ev_frame, E, fr);
+  if (r == RB_OK) r = read_rows(b, b->ds.ev_handle, E, hd);
+  if (r == RB_OK) r = read_rows(b, b->ds.ev_local, E, lo);
+  if (r == RB_OK) r = read_rows(b, b->ds.ev_remote, E, ro);
+  if (r != RB_OK) return r;
+  for (int s = 0; s < b->S; ++s) {
+    const uint32_t cnt = n[s], kept = cnt < E ? cnt : static_cast<uint32_t>(E);
+    if (counts) counts[s] = cnt;
+    for (size_t e = 0; e < E; ++e) {  // oldest kept first
+      const bool has = e < kept;
+      const size_t q = (cnt - kept + e) % E, o = static_cast<size_t>(s) * E + e;
+      if (frames) frames[o] = has ? fr[q * Sp + s] : kNullFrame;
+      if (handles) handles[o] = has ? hd[q * Sp + s] : -1;
+      if (local_checksums) local_checksums[o] = has ? lo[q * Sp + s] : 0;
+      if (remote_checksums) remote_checksums[o] = has ? ro[q * Sp + s] : 0;
+    }
+  }
+  return RB_OK;
+}
+
+rb_status rb_p2p_debug_corrupt(rb_p2p* b, int32_t session, int32_t word, uint32_t xor_mask) {
+  if (session < 0 || session >= b->S || word < 0 || word >= b->ops->canon_words)
+    return pfail(b, RB_INVALID_REQUEST, "rb_p2p_debug_corrupt: session or word out of range");
+  int lane = 0, w = 0;
+  b->ops->word_loc(word, &lane, &w);
+  const int L = b->ops->lanes, NW = b->ops->nw;
+  const size_t idx = word_index(NW, b->Spad * L, session * L + lane, w);
+  P2P_TRY(b, hipSetDevice(b->device));
+  P2P_TRY(b, hipStreamSynchronize(b->stream));
+  const size_t plane = static_cast<size_t>(NW) * b->Spad * L;
+  std::vector<uint32_t*> where{b->live + idx};
+  for (int k = 0; k < b->W; ++k) where.push_back(b->snap + k * plane + idx);
+  for (uint32_t* q : where) {
+    uint32_t v = 0;
+    P2P_TRY(b, hipMemcpy(&v, q, 4, hipMemcpyDeviceToHost));
+    v ^= xor_mask;
+    P2P_TRY(b, hipMemcpy(q, &v, 4, hipMemcpyHostToDevice));
   }
   return RB_OK;
 }

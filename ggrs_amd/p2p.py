@@ -49,6 +49,7 @@ class P2PSession:
         self.remote_delay = int(cfg.remote_delay)
         self.sparse_saving = bool(cfg.sparse_saving)
         self.local_mask = int(cfg.local_mask)
+        self.desync_interval = int(cfg.desync_interval)
         self.state_bytes = lib.rb_p2p_state_bytes(handle)
         self.input_dtype = INPUT_DTYPE[game]
         self._keep = []
@@ -158,6 +159,52 @@ class P2PSession:
         c = (ctypes.c_uint64 * 5)()
         self._check(self._lib.rb_p2p_totals(self._h, c))
         return tuple(int(x) for x in c)
+
+    # -- desync detection (p2p_session.rs:873-928)
+    def take_checksum_reports(self, out=None):
+        """The ChecksumReports every session sent since the last call, oldest
+        first, as a CUDA int64 tensor [RB_P2P_REPORTS_PER_TAKE, S, 3] (one
+        rb_checksum_report per row: checksum lo, hi, frame | mismatch << 32;
+        frame NULL_FRAME = none).  Stream-ordered; `out` may be reused."""
+        import torch
+        from .shard import REPORT_WORDS
+        K = L.RB_P2P_REPORTS_PER_TAKE
+        if out is None:
+            out = torch.empty((K, self.num_sessions, REPORT_WORDS), dtype=torch.int64, device="cuda")
+        assert out.is_cuda and out.is_contiguous() and tuple(out.shape) == (K, self.num_sessions, REPORT_WORDS)
+        self._check(self._lib.rb_p2p_take_checksum_reports(self._h, ctypes.c_void_p(out.data_ptr())))
+        return out
+
+    def receive_checksum_reports(self, handle: int, reports) -> None:
+        """The peer behind remote `handle` sent `reports` ([K, S, 3] int64 CUDA
+        tensor, take_checksum_reports layout): UdpProtocol::on_checksum_report."""
+        r, keep = _dev_ptr(reports)
+        assert keep.dim() == 3 and keep.shape[1] == self.num_sessions
+        self._keep = [keep]
+        st = self._lib.rb_p2p_receive_checksum_reports(self._h, int(handle), r, int(keep.shape[0]))
+        if st == L.RB_INVALID_REQUEST:
+            raise InvalidRequest((self._lib.rb_p2p_last_error(self._h) or b"").decode())
+        self._check(st)
+
+    def desync_events(self):
+        """(counts [S], frames [S, E], handles [S, E], local [S, E], remote [S, E]):
+        GGRSEvent::DesyncDetected per session since create, the newest E in order."""
+        E = L.RB_P2P_EVENTS_KEPT
+        n = np.empty(self.num_sessions, np.uint32)
+        fr = np.empty((self.num_sessions, E), np.int32)
+        hd = np.empty((self.num_sessions, E), np.int32)
+        lo = np.empty((self.num_sessions, E), np.uint64)
+        ro = np.empty((self.num_sessions, E), np.uint64)
+        p = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+        self._check(self._lib.rb_p2p_read_desync_events(self._h, p(n), p(fr), p(hd), p(lo), p(ro)))
+        return n, fr, hd, lo, ro
+
+    def debug_corrupt(self, session: int, word: int, xor_mask: int) -> None:
+        """Flip canonical state word `word` of the live state and every cell of `session`."""
+        st = self._lib.rb_p2p_debug_corrupt(self._h, int(session), int(word), ctypes.c_uint32(xor_mask & 0xFFFFFFFF))
+        if st == L.RB_INVALID_REQUEST:
+            raise InvalidRequest((self._lib.rb_p2p_last_error(self._h) or b"").decode())
+        self._check(st)
 
     def profile_enable(self, on: bool) -> None:
         self._check(self._lib.rb_p2p_profile_enable(self._h, int(on)))

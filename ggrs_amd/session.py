@@ -238,6 +238,13 @@ class SessionBuilder:
         self._fanout = bool(on)
         return self
 
+    def with_desync_detection_mode(self, interval: int) -> "SessionBuilder":  # builder.rs:167-172
+        """P2P: DesyncDetection::On{interval} for interval > 0, Off for 0 (default)."""
+        if interval < 0:
+            raise InvalidRequest("desync detection interval must be >= 0")
+        self._desync = int(interval)
+        return self
+
     def with_remote_input_delay(self, delay: int) -> "SessionBuilder":
         """Frame of each remote handle's first input (the peers' input delay)."""
         self._remote_delay = int(delay)
@@ -269,6 +276,7 @@ class SessionBuilder:
         pc.flags = (self._cfg.flags & L.RB_FLAG_LANE_PER_SESSION) | (
             L.RB_P2P_FLAG_FANOUT if getattr(self, "_fanout", False) else 0)
         pc.block_size = self._cfg.block_size
+        pc.desync_interval = getattr(self, "_desync", 0)
         h = ctypes.c_void_p()
         st = lib.rb_p2p_create(ctypes.byref(pc), ctypes.byref(h))
         if st != L.RB_OK:

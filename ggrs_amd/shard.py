@@ -103,3 +103,36 @@ def audit_compare(gathered, world: int, owned: int, audit: int):
     detail = torch.stack([sid, frame(own), own[:, 0], rep[:, 0]], 1) if idx.numel() else \
         torch.zeros((0, 4), dtype=torch.int64, device=gathered.device)
     return bad.sum(), detail
+
+
+# ---------------------------------------------------------------------------- P2P ChecksumReports
+def p2p_reports_to_rows(frames: np.ndarray, checksums: np.ndarray) -> np.ndarray:
+    """[K, S] frames + [K, S, 2] u128 (lo, hi) -> [K, S, 3] int64 rows in the
+    rb_checksum_report layout rb_p2p_take_checksum_reports writes."""
+    r = np.zeros(frames.shape, REPORT_DTYPE)
+    r["checksum_lo"] = checksums[..., 0]
+    r["checksum_hi"] = checksums[..., 1]
+    r["frame"] = frames
+    r["mismatch_frame"] = NULL_FRAME
+    return r.view(np.int64).reshape(frames.shape + (REPORT_WORDS,))
+
+
+def p2p_rows_to_reports(rows: np.ndarray):
+    """Inverse of p2p_reports_to_rows: (frames [K, S] i32, checksums [K, S, 2] u64)."""
+    r = np.ascontiguousarray(rows).reshape(-1, REPORT_WORDS).view(REPORT_DTYPE).reshape(rows.shape[:-1])
+    return r["frame"].copy(), np.stack([r["checksum_lo"], r["checksum_hi"]], -1)
+
+
+def exchange_checksum_reports(local, group=None):
+    """The ChecksumReport exchange of P2P desync detection on one node: every
+    rank contributes the [K, S, 3] reports its peers' batch sent this tick
+    (rb_p2p_take_checksum_reports) and receives everybody's as [world, K, S, 3];
+    a rank holding peer B of a session hands rank(peer A)'s slice to
+    rb_p2p_receive_checksum_reports.  One RCCL all-gather over xGMI (gloo on
+    the CPU tests) replaces the datagrams UdpProtocol::send_checksum_report
+    sends (protocol.rs:736-742)."""
+    flat = local.reshape(-1, local.shape[-1])
+    g = gather_reports(flat.contiguous(), group)
+    import torch.distributed as dist
+    return g.view((dist.get_world_size(group),) + tuple(local.shape))
+

@@ -225,7 +225,9 @@ typedef struct rb_p2p_config {
   int32_t sparse_saving;  /* with_sparse_saving_mode (builder.rs:159-166) */
   uint32_t flags;         /* RB_FLAG_LANE_PER_SESSION, RB_P2P_FLAG_FANOUT */
   uint32_t block_size;
-  uint32_t reserved[4];
+  int32_t desync_interval; /* with_desync_detection_mode (builder.rs:167-172): DesyncDetection::On{interval}
+                              for interval > 0, Off for 0 (the default, builder.rs:15) */
+  uint32_t reserved[3];
 } rb_p2p_config;
 
 /* Speculative branch fan-out (BASELINE config 4): after every tick each session
@@ -293,6 +295,44 @@ rb_status rb_p2p_counters(rb_p2p* b, uint32_t* out3);
  * excluded), [3] rollbacks replaced by a speculative select, [4] branch frames
  * presimulated by the fan-out. */
 rb_status rb_p2p_totals(rb_p2p* b, uint64_t* out5);
+/* ---- Desync detection (p2p_session.rs:873-928, protocol.rs:27, 710-742) with
+ * desync_interval > 0.  In every advance_frame at current % interval == 0 a
+ * session records ChecksumReport{checksum, frame = last_saved_frame - 1} of its
+ * cell (only when that frame > max_prediction; no such cell is a reference
+ * panic -> RB_PANIC), keeps it in its local checksum history (the newest 32
+ * frames), and compares the history each remote endpoint received with it:
+ * every differing frame is a GGRSEvent::DesyncDetected{frame, local_checksum,
+ * remote_checksum, addr}.  The reports travel between peers through the caller
+ * (on one node: an all-gather, ggrs_amd/shard.py), like the datagrams
+ * UdpProtocol::send_checksum_report sends. */
+#define RB_P2P_REPORTS_PER_TAKE 8 /* reports kept per session between two takes (older ones are dropped, like lost datagrams) */
+#define RB_P2P_EVENTS_KEPT 16     /* newest DesyncDetected events kept per session */
+
+/* The reports every session sent since the last call, oldest first, into
+ * device memory dev_out[RB_P2P_REPORTS_PER_TAKE][S] rb_checksum_report
+ * (frame RB_NULL_FRAME: none; mismatch_frame unused, RB_NULL_FRAME).
+ * Stream-ordered. */
+rb_status rb_p2p_take_checksum_reports(rb_p2p* b, void* dev_out);
+
+/* UdpProtocol::on_checksum_report (protocol.rs:710-722) for the endpoint of
+ * remote handle `handle` of every session: dev_in[k * S + s], k < count,
+ * rb_checksum_report in the layout rb_p2p_take_checksum_reports writes (the
+ * peer's reports for this session), applied in order.  Stream-ordered.
+ * RB_INVALID_REQUEST: handle is not a remote handle, or desync detection is off. */
+rb_status rb_p2p_receive_checksum_reports(rb_p2p* b, int32_t handle, const void* dev_in, int32_t count);
+
+/* DesyncDetected events per session: counts[S] since create, and the newest
+ * RB_P2P_EVENTS_KEPT in order as frames / remote handles (the `addr`) / local /
+ * remote checksum low words, each [S][RB_P2P_EVENTS_KEPT] (frame RB_NULL_FRAME,
+ * handle -1: none).  Any pointer may be NULL.  Synchronises. */
+rb_status rb_p2p_read_desync_events(rb_p2p* b, uint32_t* counts, int32_t* frames, int32_t* handles,
+                                    uint64_t* local_checksums, uint64_t* remote_checksums);
+
+/* Fault injection for tests (ex_game.rs:211-215 trigger_desync, generalised):
+ * XOR `xor_mask` into canonical state word `word` of `session`'s live state
+ * and of every cell it holds (checksums unchanged), between ticks. */
+rb_status rb_p2p_debug_corrupt(rb_p2p* b, int32_t session, int32_t word, uint32_t xor_mask);
+
 /* HIP event timing of every rb_p2p_run_ticks launch (bench.py): total ms and launches since the last take. */
 rb_status rb_p2p_profile_enable(rb_p2p* b, int32_t on);
 rb_status rb_p2p_profile_take(rb_p2p* b, double* total_ms, int32_t* launches);

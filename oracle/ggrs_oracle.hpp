@@ -497,12 +497,49 @@ class P2PSession {
   Frame disconnect_frame = NULL_FRAME;
   std::map<PlayerHandle, PlayerInput<I>> local_inputs;
 
+  // Desync detection (p2p_session.rs:154-157, 313-316, 873-928).
+  // DesyncDetection::On{interval} with interval > 0; 0 = Off (builder.rs:15
+  // DEFAULT_DETECTION_MODE).  Each remote handle is its own endpoint here, so
+  // the UdpProtocol side of the exchange (protocol.rs:176-178, 710-742) is
+  // one RemoteChecksums per remote handle.
+  static constexpr size_t MAX_CHECKSUM_HISTORY_SIZE = 32;  // protocol.rs:27
+  uint32_t desync_interval = 0;
+  std::unordered_map<Frame, u128> local_checksum_history;  // :157
+  struct RemoteChecksums {                                  // UdpProtocol::checksum_history et al.
+    std::unordered_map<Frame, u128> checksum_history;       // protocol.rs:177
+    Frame last_added_checksum_frame = NULL_FRAME;           // protocol.rs:178
+  };
+  std::vector<RemoteChecksums> remote_checksums;           // [num_players], remote handles only
+  std::vector<std::pair<Frame, u128>> sent_reports;        // ChecksumReport messages sent, in order
+  struct DesyncEvent {                                      // GGRSEvent::DesyncDetected (lib.rs:157-166)
+    Frame frame;
+    u128 local_checksum, remote_checksum;
+    PlayerHandle handle;  // stands for `addr`: the remote endpoint
+  };
+  std::vector<DesyncEvent> events;
+
   // :160-213 (local players get the input delay; remote queues have none)
   P2PSession(size_t np, size_t mp, bool sparse, size_t delay, std::vector<bool> local)
       : num_players(np), max_prediction(mp), sparse_saving(sparse), sync_layer(np, mp),
-        local_connect_status(np), is_local(std::move(local)) {
+        local_connect_status(np), is_local(std::move(local)), remote_checksums(np) {
     for (size_t h = 0; h < np; ++h)
       if (is_local[h]) sync_layer.set_frame_delay(h, delay);
+  }
+
+  // UdpProtocol::on_checksum_report (protocol.rs:710-722) of remote handle h's
+  // endpoint: a ChecksumReport{checksum, frame} arrived from that peer.
+  void on_checksum_report(PlayerHandle h, Frame frame, u128 checksum) {
+    ORC_ASSERT(h < num_players && !is_local[h]);
+    auto& r = remote_checksums[h];
+    if (r.last_added_checksum_frame < frame) {
+      if (r.checksum_history.size() > MAX_CHECKSUM_HISTORY_SIZE) {
+        const Frame keep_after = r.last_added_checksum_frame - static_cast<Frame>(MAX_CHECKSUM_HISTORY_SIZE);
+        for (auto it = r.checksum_history.begin(); it != r.checksum_history.end();)
+          it = it->first > keep_after ? std::next(it) : r.checksum_history.erase(it);
+      }
+      r.last_added_checksum_frame = frame;
+      r.checksum_history[frame] = checksum;
+    }
   }
 
   Error add_local_input(PlayerHandle h, I input) {  // :223-240
@@ -560,6 +597,10 @@ class P2PSession {
     else
       requests.push_back(sync_layer.save_current_state());
     sync_layer.set_last_confirmed_frame(confirmed, sparse_saving);
+    if (desync_interval) {  // :313-316
+      check_checksum_send_interval();
+      compare_local_checksums_against_peers();
+    }
     for (size_t h = 0; h < num_players; ++h) {  // local_player_handles()
       if (!is_local[h]) continue;
       auto it = local_inputs.find(h);
@@ -580,6 +621,41 @@ class P2PSession {
   }
 
  private:
+  // :900-928.  The report is "sent" to every remote endpoint (sent_reports;
+  // the caller forwards it to the peers' on_checksum_report).
+  void check_checksum_send_interval() {
+    const Frame frame_to_send = sync_layer.last_saved_frame - 1;
+    const Frame current = current_frame();
+    if (current % static_cast<Frame>(desync_interval) == 0 && frame_to_send > static_cast<Frame>(max_prediction)) {
+      auto cell = sync_layer.saved_state_by_frame(frame_to_send);
+      if (!cell) throw Panic("cell not found!: frame " + std::to_string(frame_to_send));
+      if (auto checksum = cell->checksum()) {
+        sent_reports.push_back({frame_to_send, *checksum});
+        local_checksum_history[frame_to_send] = *checksum;
+      }
+    }
+    if (local_checksum_history.size() > MAX_CHECKSUM_HISTORY_SIZE) {
+      const Frame keep_after = current - static_cast<Frame>(MAX_CHECKSUM_HISTORY_SIZE);
+      for (auto it = local_checksum_history.begin(); it != local_checksum_history.end();)
+        it = it->first > keep_after ? std::next(it) : local_checksum_history.erase(it);
+    }
+  }
+  // :873-898.  The reference walks HashMaps (unspecified order); here the
+  // remote handles ascend and each endpoint's history is walked by frame.
+  void compare_local_checksums_against_peers() {
+    if (current_frame() % static_cast<Frame>(desync_interval) != 0) return;
+    for (size_t h = 0; h < num_players; ++h) {
+      if (is_local[h]) continue;
+      std::map<Frame, u128> ordered(remote_checksums[h].checksum_history.begin(),
+                                    remote_checksums[h].checksum_history.end());
+      for (auto& [remote_frame, remote_checksum] : ordered) {
+        auto it = local_checksum_history.find(remote_frame);
+        if (it != local_checksum_history.end() && it->second != remote_checksum)
+          events.push_back({remote_frame, it->second, remote_checksum, h});
+      }
+    }
+  }
+
   void adjust_gamestate(Frame first_incorrect, Frame min_confirmed, std::vector<Request<C>>& requests) {  // :621-673
     Frame current = sync_layer.current_frame();
     Frame frame_to_load = sparse_saving ? sync_layer.last_saved_frame : first_incorrect;

@@ -62,6 +62,11 @@ def load():
             "orc_p2p_read_cells": (I32, [P, P, P, P]),
             "orc_p2p_read_live": (I32, [P, P, P]),
             "orc_p2p_frames": (I32, [P, P, P]),
+            "orc_p2p_set_desync": (None, [P, ctypes.c_uint32]),
+            "orc_p2p_take_reports": (I32, [P, P, P, I32]),
+            "orc_p2p_receive_reports": (I32, [P, I32, P, P, I32]),
+            "orc_p2p_events": (I32, [P, P, P, P, P, P, I32]),
+            "orc_p2p_corrupt": (I32, [P, I32, I32, ctypes.c_uint32]),
             "orc_wire_encode": (I32, [P, I32, P, I32, P, I32]),
             "orc_bench_p2p_exgame": (ctypes.c_double, [I32, I32, I32, ctypes.c_uint32, I32, I32, I32, I32, I32, P,
                                                         P, P, I32, P, P]),
@@ -230,6 +235,40 @@ class OracleP2P:
         k = np.empty(self.S, np.int32)
         self._lib.orc_p2p_frames(self._h, _ptr(c), _ptr(k))
         return c, k
+
+    # -- desync detection (p2p_session.rs:873-928)
+    def set_desync_detection(self, interval: int) -> None:
+        """DesyncDetection::On{interval} (0 = Off)."""
+        self._lib.orc_p2p_set_desync(self._h, int(interval))
+
+    def take_checksum_reports(self, K: int = 8):
+        """ChecksumReports sent since the last call, oldest first: (frames [K, S]
+        (NULL_FRAME = none), checksums [K, S, 2] u128 lo/hi)."""
+        fr = np.empty((K, self.S), np.int32)
+        cs = np.empty((K, self.S, 2), np.uint64)
+        self._lib.orc_p2p_take_reports(self._h, _ptr(fr), _ptr(cs), K)
+        return fr, cs
+
+    def receive_checksum_reports(self, handle: int, frames, checksums) -> int:
+        """The peer of remote `handle` sent these reports (take_checksum_reports layout)."""
+        fr = np.ascontiguousarray(frames, np.int32)
+        cs = np.ascontiguousarray(checksums, np.uint64)
+        return self._lib.orc_p2p_receive_reports(self._h, handle, _ptr(fr), _ptr(cs), fr.shape[0])
+
+    def desync_events(self, E: int = 16):
+        """(counts [S], frames [S, E], handles [S, E], local [S, E], remote [S, E]):
+        DesyncDetected events since create, the newest E of each session in order."""
+        n = np.empty(self.S, np.uint32)
+        fr = np.empty((self.S, E), np.int32)
+        hd = np.empty((self.S, E), np.int32)
+        lo = np.empty((self.S, E), np.uint64)
+        ro = np.empty((self.S, E), np.uint64)
+        self._lib.orc_p2p_events(self._h, _ptr(n), _ptr(fr), _ptr(hd), _ptr(lo), _ptr(ro), E)
+        return n, fr, hd, lo, ro
+
+    def corrupt(self, session: int, word: int, xor_mask: int) -> None:
+        """Flip canonical state word `word` of the live state and every saved cell."""
+        self._lib.orc_p2p_corrupt(self._h, session, word, xor_mask & 0xFFFFFFFF)
 
 
 def fletcher16(data: bytes) -> int:

@@ -72,6 +72,9 @@ inline void corrupt_state(stub::StateStub& st, int32_t, uint32_t m) { st.state ^
 inline void corrupt_state(stub::StateStubEnum& st, int32_t, uint32_t m) { st.state ^= static_cast<int32_t>(m); }
 template <class G>
 inline const auto& live_of(const G& g) { return g.gs; }
+inline exgame::State& mutable_live(exgame::Game& g) { return g.game_state; }
+template <class G>
+inline auto& mutable_live(G& g) { return g.gs; }
 
 template <class C, class G>
 struct Batch : BatchBase {
@@ -205,6 +208,13 @@ struct P2PBatchBase {
   virtual int32_t read_cells(int32_t* cell_frames, uint8_t* images, uint64_t* cs) = 0;
   virtual int32_t read_live(uint8_t* images, int32_t* frames) = 0;
   virtual int32_t frames(int32_t* current, int32_t* confirmed) = 0;
+  // desync detection (p2p_session.rs:873-928)
+  virtual void set_desync(uint32_t interval) = 0;
+  virtual int32_t take_reports(int32_t* frames, uint64_t* cs, int32_t K) = 0;
+  virtual int32_t receive_reports(int32_t handle, const int32_t* frames, const uint64_t* cs, int32_t K) = 0;
+  virtual int32_t events(uint32_t* counts, int32_t* frames, int32_t* handles, uint64_t* local, uint64_t* remote,
+                         int32_t E) = 0;
+  virtual int32_t corrupt(int32_t session, int32_t word, uint32_t mask) = 0;
   std::string last_panic;
 };
 
@@ -228,13 +238,19 @@ struct P2PBatch : P2PBatchBase {
       games.push_back(mk(s));
     }
     last_reqs.resize(S);
+    panicked.assign(S, false);
   }
+  // A reference panic aborts the process; a batch freezes the session that hit
+  // it and keeps reporting the panic (the device does the same).
+  std::vector<bool> panicked;
 
   int32_t deliver(int32_t handle, const int32_t* upto, const uint8_t* by_frame, int32_t n_frames) override {
     const size_t S = sess.size();
-    try {
-      for (size_t s = 0; s < S; ++s) {
-        auto& ss = *sess[s];
+    int32_t rc = 0;
+    for (size_t s = 0; s < S; ++s) {
+      if (panicked[s]) continue;
+      auto& ss = *sess[s];
+      try {  // poll_remote_clients: a reference assert here panics this session only
         Frame last = ss.local_connect_status.at(handle).last_frame;
         Frame f0 = last == NULL_FRAME ? remote_first : last + 1;
         for (Frame f = f0; f <= upto[s]; ++f) {
@@ -243,17 +259,20 @@ struct P2PBatch : P2PBatchBase {
           std::memcpy(&v, by_frame + (static_cast<size_t>(f) * S + s) * sizeof(I), sizeof(I));
           ss.deliver_remote_input(static_cast<PlayerHandle>(handle), PlayerInput<I>(f, v));
         }
+      } catch (const Panic& p) {
+        last_panic = p.what();
+        panicked[s] = true;
+        last_reqs[s].clear();
+        rc = KIND_PANIC;
       }
-    } catch (const Panic& p) {
-      last_panic = p.what();
-      return KIND_PANIC;
     }
-    return 0;
+    return rc;
   }
 
   int32_t add_local_input(int32_t handle, const uint8_t* in) override {
     int32_t first = 0;
     for (size_t s = 0; s < sess.size(); ++s) {
+      if (panicked[s]) continue;
       I v{};
       std::memcpy(&v, in + s * sizeof(I), sizeof(I));
       Error e = sess[s]->add_local_input(static_cast<PlayerHandle>(handle), v);
@@ -267,7 +286,7 @@ struct P2PBatch : P2PBatchBase {
   int32_t disconnect(int32_t handle, const uint8_t* mask) override {
     int32_t first = 0;
     for (size_t s = 0; s < sess.size(); ++s) {
-      if (mask && !mask[s]) continue;
+      if ((mask && !mask[s]) || panicked[s]) continue;
       Error e = sess[s]->disconnect_player(static_cast<PlayerHandle>(handle));
       if (e.is_err() && first == 0) first = static_cast<int32_t>(e.kind);
     }
@@ -278,7 +297,9 @@ struct P2PBatch : P2PBatchBase {
     int32_t nerr = 0;
     for (size_t s = 0; s < sess.size(); ++s) {
       int32_t k = 0;
-      try {
+      if (panicked[s]) {
+        k = KIND_PANIC;
+      } else try {
         Error e = sess[s]->advance_frame(last_reqs[s]);
         if (e.is_err()) k = static_cast<int32_t>(e.kind);
         // on Err the requests built before the failure stay in the Vec the
@@ -289,6 +310,7 @@ struct P2PBatch : P2PBatchBase {
       } catch (const Panic& p) {
         k = KIND_PANIC;
         last_panic = p.what();
+        panicked[s] = true;
       }
       Frame lf = NULL_FRAME;
       int32_t na = 0, ns = 0;
@@ -354,6 +376,83 @@ struct P2PBatch : P2PBatchBase {
     for (size_t s = 0; s < sess.size(); ++s) {
       if (current) current[s] = sess[s]->current_frame();
       if (confirmed) confirmed[s] = sess[s]->sync_layer.last_confirmed_frame;
+    }
+    return 0;
+  }
+
+  void set_desync(uint32_t interval) override {
+    for (auto& ss : sess) ss->desync_interval = interval;
+  }
+  // The ChecksumReports each session sent since the last take, oldest first:
+  // frames [K][S] (NULL_FRAME = none), checksums [K][S][2] (u128 lo, hi).  When
+  // more than K were sent only the newest K are kept (a lost datagram).
+  int32_t take_reports(int32_t* frames, uint64_t* cs, int32_t K) override {
+    const size_t S = sess.size();
+    for (size_t s = 0; s < S; ++s) {
+      auto& r = sess[s]->sent_reports;
+      const size_t n = r.size(), first = n > static_cast<size_t>(K) ? n - K : 0;
+      for (int32_t k = 0; k < K; ++k) {
+        const size_t i = first + static_cast<size_t>(k);
+        const bool has = i < n;
+        frames[k * S + s] = has ? r[i].first : NULL_FRAME;
+        cs[(k * S + s) * 2 + 0] = has ? static_cast<uint64_t>(r[i].second) : 0;
+        cs[(k * S + s) * 2 + 1] = has ? static_cast<uint64_t>(r[i].second >> 64) : 0;
+      }
+      r.clear();
+    }
+    return 0;
+  }
+  // The peer's reports for remote handle `handle`, in the same layout, applied
+  // in order by UdpProtocol::on_checksum_report.
+  int32_t receive_reports(int32_t handle, const int32_t* frames, const uint64_t* cs, int32_t K) override {
+    const size_t S = sess.size();
+    try {
+      for (size_t s = 0; s < S; ++s) {
+        if (panicked[s]) continue;
+        for (int32_t k = 0; k < K; ++k) {
+          const Frame f = frames[k * S + s];
+          if (f == NULL_FRAME) continue;
+          const u128 c = (static_cast<u128>(cs[(k * S + s) * 2 + 1]) << 64) | cs[(k * S + s) * 2 + 0];
+          sess[s]->on_checksum_report(static_cast<PlayerHandle>(handle), f, c);
+        }
+      }
+    } catch (const Panic& p) {
+      last_panic = p.what();
+      return KIND_PANIC;
+    }
+    return 0;
+  }
+  // DesyncDetected events: total per session, and the newest E in order
+  // (frames [S][E] NULL_FRAME-padded, remote handle, local/remote checksum low words).
+  int32_t events(uint32_t* counts, int32_t* frames, int32_t* handles, uint64_t* local, uint64_t* remote,
+                 int32_t E) override {
+    for (size_t s = 0; s < sess.size(); ++s) {
+      auto& ev = sess[s]->events;
+      const size_t n = ev.size(), first = n > static_cast<size_t>(E) ? n - E : 0;
+      if (counts) counts[s] = static_cast<uint32_t>(n);
+      for (int32_t e = 0; e < E; ++e) {
+        const size_t i = first + static_cast<size_t>(e);
+        const bool has = i < n;
+        const size_t o = s * E + e;
+        if (frames) frames[o] = has ? ev[i].frame : NULL_FRAME;
+        if (handles) handles[o] = has ? static_cast<int32_t>(ev[i].handle) : -1;
+        if (local) local[o] = has ? static_cast<uint64_t>(ev[i].local_checksum) : 0;
+        if (remote) remote[o] = has ? static_cast<uint64_t>(ev[i].remote_checksum) : 0;
+      }
+    }
+    return 0;
+  }
+  // Fault injection (ex_game.rs:211-215 trigger_desync, generalised): flip
+  // word `word` of the session's live game state and of every saved cell's
+  // state (cell checksums unchanged), so no rollback can undo it.
+  int32_t corrupt(int32_t session, int32_t word, uint32_t mask) override {
+    auto& ss = *sess.at(static_cast<size_t>(session));
+    corrupt_state(mutable_live(games[static_cast<size_t>(session)]), word, mask);
+    for (auto& cell : ss.sync_layer.saved_states.states) {
+      auto d = cell.load();
+      if (!d || cell.frame() == NULL_FRAME) continue;
+      corrupt_state(*d, word, mask);
+      cell.save(cell.frame(), *d, cell.checksum());
     }
     return 0;
   }
@@ -469,6 +568,20 @@ int32_t orc_p2p_read_live(void* b, uint8_t* images, int32_t* frames) {
 }
 int32_t orc_p2p_frames(void* b, int32_t* current, int32_t* confirmed) {
   return static_cast<P2PBatchBase*>(b)->frames(current, confirmed);
+}
+void orc_p2p_set_desync(void* b, uint32_t interval) { static_cast<P2PBatchBase*>(b)->set_desync(interval); }
+int32_t orc_p2p_take_reports(void* b, int32_t* frames, uint64_t* cs, int32_t K) {
+  return static_cast<P2PBatchBase*>(b)->take_reports(frames, cs, K);
+}
+int32_t orc_p2p_receive_reports(void* b, int32_t handle, const int32_t* frames, const uint64_t* cs, int32_t K) {
+  return static_cast<P2PBatchBase*>(b)->receive_reports(handle, frames, cs, K);
+}
+int32_t orc_p2p_events(void* b, uint32_t* counts, int32_t* frames, int32_t* handles, uint64_t* local, uint64_t* remote,
+                       int32_t E) {
+  return static_cast<P2PBatchBase*>(b)->events(counts, frames, handles, local, remote, E);
+}
+int32_t orc_p2p_corrupt(void* b, int32_t session, int32_t word, uint32_t mask) {
+  return static_cast<P2PBatchBase*>(b)->corrupt(session, word, mask);
 }
 
 // network/compression.rs wire format (ggrs_oracle.hpp namespace wire).

@@ -204,3 +204,45 @@ def test_bench_rehearsal_audit_reports_an_injected_desync():
     rep = d["config"]["desync_reports"]
     assert rep["ranks"] == 3 and rep["audit_desynced"] == 1
     assert rep["first_desync"][:2] == [256, 9]  # rank 0's replica of global session 256 (rank 1's first), frame 9
+
+
+def _p2p_peer_rank(rank, world, port, outdir):
+    # rank 0 holds peer A (handle 0 local) of every session, rank 1 peer B:
+    # the two views of the same sessions on two ranks, their ChecksumReports
+    # exchanged by the all-gather every tick.  Rank 0 flips three sessions.
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ggrs_amd.p2p import synth_network
+        S, P2, T, d, interval = 32, 2, 90, 2, 10
+        mask = 0b01 if rank == 0 else 0b10
+        inputs, upto, rin = synth_network(S, P2, T, mask, d, 0, 1)
+        orc = O.OracleP2P(O.EX_GAME, P2, 8, d, mask, S, remote_delay=d)
+        orc.set_desync_detection(interval)
+        remote = 1 - rank  # this peer's remote handle = the other rank's local one
+        for t in range(T):
+            if t == 41 and rank == 0:
+                for s in (4, 19, 30):
+                    orc.corrupt(s, 4 * P2, 0x00100000)
+            orc.deliver(remote, upto[t, remote], rin[:, remote, :])
+            orc.add_local_input(rank, inputs[t, rank])
+            assert (orc.advance()[0] == 0).all()
+            fr, cs = orc.take_checksum_reports(8)
+            g = shard.exchange_checksum_reports(torch.from_numpy(shard.p2p_reports_to_rows(fr, cs)))
+            pf, pc = shard.p2p_rows_to_reports(g[1 - rank].numpy())
+            assert orc.receive_checksum_reports(remote, pf, pc) == 0
+        n, fr, hd, lo, ro = orc.desync_events()
+        np.save(os.path.join(outdir, f"events{rank}.npy"), n)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_gloo_p2p_checksum_exchange_detects_desync():
+    port = _free_port()
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_p2p_peer_rank, args=(2, port, d), nprocs=2, join=True)
+        n0 = np.load(os.path.join(d, "events0.npy"))
+        n1 = np.load(os.path.join(d, "events1.npy"))
+    # both peers raise DesyncDetected on exactly the flipped sessions
+    assert np.nonzero(n0)[0].tolist() == [4, 19, 30]
+    assert np.nonzero(n1)[0].tolist() == [4, 19, 30]
