@@ -136,16 +136,42 @@ struct P2PParams {
   DesyncParams ds;
 };
 
+// The cells as check_checksum_send_interval sees them.  It runs inside
+// advance_frame, before the user executes the requests that advance_frame
+// returns, so the cell it reads (frame last_saved_frame - 1) carries what the
+// requests of EARLIER ticks saved, not this tick's rollback saves.  The
+// device executes a tick's saves as it goes, so the lead lane snapshots the
+// cells the send can read before the tick's rollback: the frame saved last is
+// the current frame, the confirmed frame (sparse adjust) or the previous
+// last saved frame, so frame_to_send is one of those minus one.
+struct CellSnap {
+  int32_t frame[3], tag[3];
+  uint64_t cs[3];
+};
+template <class CS>
+__device__ __forceinline__ CellSnap snap_send_cells(const CS* __restrict__ cs, const int32_t* __restrict__ tag, unsigned s,
+                                                    unsigned Spad, int32_t W, int32_t cur, int32_t confirmed,
+                                                    int32_t last_saved) {
+  CellSnap c;
+  const int32_t f[3] = {cur - 1, confirmed - 1, last_saved - 1};
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    c.frame[k] = f[k];
+    const unsigned slot = static_cast<unsigned>(f[k] >= 0 ? f[k] % W : 0);
+    c.tag[k] = f[k] >= 0 ? tag[slot * Spad + s] : kNullFrame;
+    c.cs[k] = to_u128(cs[slot * Spad + s]).lo;  // P2P games' checksums are < 2^64
+  }
+  return c;
+}
+
 // check_checksum_send_interval + compare_local_checksums_against_peers
 // (p2p_session.rs:873-928) for session s at current frame `cur`, after
 // set_last_confirmed_frame (:306-316).  Lead lane only.  Returns false when the
 // reference would panic ("cell not found!", :907-910).  The compare walks the
 // remote handles in ascending order and each history in frame order (the
 // reference iterates HashMaps; the order of its events is unspecified).
-template <class CS>
-__device__ __noinline__ bool desync_step(const DesyncParams& d, const CS* __restrict__ cs, const int32_t* __restrict__ tag,
-                                         unsigned s, unsigned Spad, int32_t cur, int32_t last_saved, int32_t W,
-                                         int P, uint32_t local_mask) {
+__device__ __noinline__ bool desync_step(const DesyncParams& d, const CellSnap& cells, unsigned s, unsigned Spad,
+                                         int32_t cur, int32_t last_saved, int32_t W, int P, uint32_t local_mask) {
   if (cur % d.interval != 0) return true;  // both steps act on interval frames only
   auto at = [&](int k) { return static_cast<size_t>(k) * Spad + s; };
   int32_t lf[kCsHist];
@@ -153,9 +179,13 @@ __device__ __noinline__ bool desync_step(const DesyncParams& d, const CS* __rest
   for (int k = 0; k < kCsHist; ++k) lf[k] = d.lh_frame[at(k)];
   const int32_t frame_to_send = last_saved - 1;
   if (frame_to_send > W) {
-    const unsigned slot = static_cast<unsigned>(frame_to_send % W);
-    if (tag[slot * Spad + s] != frame_to_send) return false;  // saved_state_by_frame(..).unwrap_or_else(panic)
-    const uint64_t c = to_u128(cs[slot * Spad + s]).lo;  // P2P games' checksums are < 2^64
+    int ci = -1;
+#pragma unroll
+    for (int k = 2; k >= 0; --k) ci = cells.frame[k] == frame_to_send ? k : ci;
+    if (ci < 0) return false;  // cannot happen (see CellSnap)
+    const int32_t ctag = ci == 0 ? cells.tag[0] : (ci == 1 ? cells.tag[1] : cells.tag[2]);
+    if (ctag != frame_to_send) return false;  // saved_state_by_frame(..).unwrap_or_else(panic)
+    const uint64_t c = ci == 0 ? cells.cs[0] : (ci == 1 ? cells.cs[1] : cells.cs[2]);
     const uint32_t n = d.ob_n[s];  // send_checksum_report to every remote endpoint
     d.ob_frame[at(static_cast<int>(n % kOutbox))] = frame_to_send;
     d.ob_cs[at(static_cast<int>(n % kOutbox))] = c;
@@ -615,12 +645,13 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
   };
   // desync detection after set_last_confirmed_frame (p2p_session.rs:313-316):
   // the lead lane runs it, the group learns whether it panicked
+  [[maybe_unused]] CellSnap send_cells{};
   auto run_desync = [&]() __attribute__((always_inline)) -> bool {
     if constexpr (!kDesync) {
       return true;
     } else {
       bool ok = true;
-      if (lead) ok = desync_step<CS>(p.ds, csa, p.tag, s, Spad, cur, last_saved, W, P, p.local_mask);
+      if (lead) ok = desync_step(p.ds, send_cells, s, Spad, cur, last_saved, W, P, p.local_mask);
       return group_min<L>(ok ? 1 : 0) == 1;
     }
   };
@@ -680,6 +711,13 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
         status = kP2PStatusPanic;
         break;
       }
+    }
+    if constexpr (kDesync) {  // the cells check_checksum_send_interval will read, before this tick's saves
+      int32_t confirmed = INT32_MAX;
+#pragma unroll
+      for (int j = 0; j < PPL; ++j) confirmed = min(confirmed, conn_of(j));
+      confirmed = group_min<L>(confirmed);  // confirmed_frame (:487-498)
+      if (lead && cur % p.ds.interval == 0) send_cells = snap_send_cells(csa, p.tag, s, Spad, W, cur, confirmed, last_saved);
     }
     // ---- PredictionThreshold (sync_layer.rs:163-167) is decided by bookkeeping
     // alone: without sparse saving from the confirmed frame, with it by a dry run.
