@@ -15,7 +15,7 @@
 //   image     host: canonical byte image of (frame, words [kLanes][NWL])
 // The cell's frame tag is stored once per slot (batch-uniform): every game
 // here asserts state.frame == cell frame on save (ex_game.rs:89,
-// stubs.rs:53,93, stubs_enum.rs:185), so the per-session frame word is
+// stubs.rs:53,93, stubs_enum.rs:59), so the per-session frame word is
 // redundant and is supplied from the tag instead of being stored S times.
 #pragma once
 
@@ -213,6 +213,7 @@ struct ExGame {
   //   up ? v + t : v - t          ==  v + (up ? t : -t)    (IEEE a - b = a + (-b))
   //   left ? rot - r : rot + r    ==  rot + (left ? -r : r)
   static constexpr bool kHasPrep = true;
+  static constexpr bool kUsesStatus = false;  // reads only Disconnected (status bit i)
   template <int N>
   struct Prep {
     float tx[kPlayersPerLane][N], ty[kPlayersPerLane][N];  // signed thrust of frame k
@@ -381,6 +382,7 @@ struct Brawler {
   // the players' new positions, then the damage the players took.
   static constexpr bool kHasRangePath = false;
   static constexpr bool kHasPrep = false;  // plain advance in the fused steady ticks
+  static constexpr bool kUsesStatus = false;
   __device__ static bool in_range(const uint32_t (&)[NWL]) { return false; }
   template <bool = false>
   __device__ static void advance(uint32_t (&w)[NWL], InRec rec, int lane, uint32_t disc, uint32_t*) {
@@ -509,6 +511,7 @@ struct StubGame {
   // stubs.rs:115-125
   static constexpr bool kHasRangePath = false;
   static constexpr bool kHasPrep = false;  // plain advance in the fused steady ticks
+  static constexpr bool kUsesStatus = false;
   __device__ static bool in_range(const uint32_t (&)[NWL]) { return false; }
   template <bool = false>
   __device__ static void advance(uint32_t (&w)[NWL], InRec rec, int, uint32_t, uint32_t*) {
@@ -537,13 +540,20 @@ struct StubEnumGame {
   static void word_loc(int, int* lane, int* word) { *lane = 0; *word = 0; }
   static constexpr int kCanonWords = 1;
   __device__ static uint32_t player_input(InRec rec, int p) { return (static_cast<uint32_t>(rec) >> (8 * p)) & 0xffu; }
-  // stubs_enum.rs:206-216
+  // StateStubEnum::advance_frame (stubs_enum.rs:80-90): `p0_inputs == p1_inputs`
+  // compares (EnumInput, InputStatus) tuples.  InputStatus of player i from the
+  // status bits: bit i Disconnected (its input is zeroed), bit 8+i Predicted.
   static constexpr bool kHasRangePath = false;
   static constexpr bool kHasPrep = false;  // plain advance in the fused steady ticks
+  static constexpr bool kUsesStatus = true;  // Predicted bits (8 + i) too
   __device__ static bool in_range(const uint32_t (&)[NWL]) { return false; }
+  __device__ static uint32_t status_of(uint32_t bits, int i) {
+    return ((bits >> i) & 1u) ? 2u : ((bits >> (8 + i)) & 1u);  // Disconnected 2, Predicted 1, Confirmed 0
+  }
   template <bool = false>
-  __device__ static void advance(uint32_t (&w)[NWL], InRec rec, int, uint32_t, uint32_t*) {
-    w[0] = (player_input(rec, 0) == player_input(rec, 1)) ? w[0] + 2u : w[0] - 1u;
+  __device__ static void advance(uint32_t (&w)[NWL], InRec rec, int, uint32_t status_bits, uint32_t*) {
+    const bool same = player_input(rec, 0) == player_input(rec, 1) && status_of(status_bits, 0) == status_of(status_bits, 1);
+    w[0] = same ? w[0] + 2u : w[0] - 1u;
   }
   __device__ static CS checksum(const uint32_t (&w)[NWL], int32_t frame, int, const CsCtx&) {
     return siphash13_i32x2(frame, static_cast<int32_t>(w[0]));

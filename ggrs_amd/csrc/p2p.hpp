@@ -483,8 +483,12 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     for (int j = 0; j < PPL; ++j) {
       const int h = player_of(j);
       if (h >= P) continue;
-      if (q[j].disc && q[j].conn_last < f) dmask |= 1u << h;
-      else rec |= static_cast<uint64_t>(q_input(q[j], ring, h, s, f)) << (8 * IB * h);
+      if (q[j].disc && q[j].conn_last < f) {
+        dmask |= 1u << h;
+      } else {
+        rec |= static_cast<uint64_t>(q_input(q[j], ring, h, s, f)) << (8 * IB * h);
+        if constexpr (G::kUsesStatus) dmask |= (q[j].pred_frame >= 0 ? 1u : 0u) << (8 + h);  // InputStatus::Predicted
+      }
     }
     return static_cast<InRec>(rec);
   };

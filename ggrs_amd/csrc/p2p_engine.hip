@@ -189,8 +189,9 @@ rb_status rb_p2p_create(const rb_p2p_config* cfg, rb_p2p** out) {
     return pfail(nullptr, RB_INVALID_REQUEST, "a P2P batch needs at least one local and one remote handle");
   if (cfg->max_prediction > 64 || cfg->input_delay + cfg->max_prediction + 2 > kQueueLen)
     return pfail(nullptr, RB_INVALID_REQUEST, "max_prediction / input delay do not fit the 128-entry input queue");
-  if (cfg->game != RB_GAME_EX_GAME && cfg->game != RB_GAME_STUB && cfg->game != RB_GAME_BRAWLER)
-    return pfail(nullptr, RB_INVALID_REQUEST, "P2P batches support ex_game, the stub game and the brawler");
+  if (cfg->game != RB_GAME_EX_GAME && cfg->game != RB_GAME_STUB && cfg->game != RB_GAME_STUB_ENUM &&
+      cfg->game != RB_GAME_BRAWLER)
+    return pfail(nullptr, RB_INVALID_REQUEST, "P2P batches support ex_game, the stub games and the brawler");
   auto ops = make_game(cfg->game, cfg->num_players, (cfg->flags & RB_FLAG_LANE_PER_SESSION) != 0);
   if (!ops) return pfail(nullptr, RB_INVALID_REQUEST, "unsupported game / num_players combination");
   const bool fanout = (cfg->flags & RB_P2P_FLAG_FANOUT) != 0;

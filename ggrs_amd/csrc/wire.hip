@@ -67,6 +67,17 @@ __global__ void __launch_bounds__(256) decode_packets_kernel(const DecParams p) 
     p.status[s] = kDecNothing;
     return;
   }
+  // recv_inputs never holds a frame below NULL_FRAME: such a packet finds no
+  // decode input and is ignored (protocol.rs:653); a reference input past the
+  // caller's remote_inputs tensor cannot be read at all
+  if (last != kNull && start - 1 < kNull) {
+    p.status[s] = kDecNothing;
+    return;
+  }
+  if (start - 1 >= p.remote_frames) {
+    p.status[s] = kDecMalformed;
+    return;
+  }
   uint8_t ref[4] = {0, 0, 0, 0};  // recv_inputs[NULL_FRAME] is the zeroed input (protocol.rs:213-214)
   if (last != kNull && start - 1 != kNull)
     for (int i = 0; i < IB; ++i) ref[i] = in_byte(p.remote_inputs, start - 1, h, p.P, p.S, s, IB, i);

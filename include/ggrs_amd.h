@@ -214,7 +214,7 @@ typedef struct rb_p2p rb_p2p;
 
 typedef struct rb_p2p_config {
   int32_t abi_version;    /* = RB_ABI_VERSION */
-  int32_t game;           /* rb_game: RB_GAME_EX_GAME, RB_GAME_STUB, RB_GAME_BRAWLER */
+  int32_t game;           /* rb_game: RB_GAME_EX_GAME, RB_GAME_STUB, RB_GAME_STUB_ENUM, RB_GAME_BRAWLER */
   int32_t num_sessions;
   int32_t num_players;    /* with_num_players (builder.rs:154-157) */
   int32_t max_prediction; /* with_max_prediction_window (builder.rs:136-145) */

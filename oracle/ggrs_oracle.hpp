@@ -981,13 +981,14 @@ struct RandomChecksumGameStub {
   }
 };
 
-// stubs_enum.rs:144-216
+// stubs_enum.rs:18-29 (EnumInput), 73-91 (StateStubEnum)
 enum class EnumInput : uint8_t { Val1 = 0, Val2 = 1 };
 struct StateStubEnum {
   int32_t frame = 0;
   int32_t state = 0;
+  // stubs_enum.rs:80-90: `p0_inputs == p1_inputs` compares (EnumInput, InputStatus) tuples
   void advance_frame(const std::vector<std::pair<EnumInput, InputStatus>>& inputs) {
-    if (inputs[0].first == inputs[1].first) state += 2; else state -= 1;
+    if (inputs[0].first == inputs[1].first && inputs[0].second == inputs[1].second) state += 2; else state -= 1;
     frame += 1;
   }
 };

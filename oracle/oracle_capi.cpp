@@ -532,6 +532,10 @@ void* orc_p2p_create(int32_t game, int32_t num_players, int32_t max_prediction, 
       case STUB:
         return new P2PBatch<stub::Config, stub::GameStub>(num_players, max_prediction, input_delay, local_mask, sp,
                                                           remote_delay, num_sessions, [&](int32_t) { return stub::GameStub{}; });
+      case STUB_ENUM:
+        return new P2PBatch<stub::EnumConfig, stub::GameStubEnum>(num_players, max_prediction, input_delay, local_mask,
+                                                                  sp, remote_delay, num_sessions,
+                                                                  [&](int32_t) { return stub::GameStubEnum{}; });
       case BRAWLER:
         return new P2PBatch<brawler::Config, brawler::Game>(num_players, max_prediction, input_delay, local_mask, sp,
                                                             remote_delay, num_sessions,

@@ -17,7 +17,7 @@ from ggrs_amd._lib import RB_PANIC
 from ggrs_amd.p2p import PlayerType, synth_network
 from oracle import oracle as O
 
-ORC_GAME = {G.Game.EX_GAME: O.EX_GAME, G.Game.STUB: O.STUB, G.Game.BRAWLER: O.BRAWLER}
+ORC_GAME = {G.Game.EX_GAME: O.EX_GAME, G.Game.STUB: O.STUB, G.Game.STUB_ENUM: O.STUB_ENUM, G.Game.BRAWLER: O.BRAWLER}
 
 
 def drive_oracle(orc, local_mask, inputs, upto, remote_in, T, t0=0, disc=None):
@@ -231,6 +231,9 @@ CASES = [  # game, P, W, d, rd, local_mask, sparse, lag range
     (G.Game.STUB, 2, 8, 1, 0, 0b01, False, (1, 5)),
     (G.Game.STUB, 2, 6, 0, 1, 0b10, True, (1, 4)),
     (G.Game.EX_GAME, 2, 4, 0, 0, 0b01, False, (1, 6)),  # lags past the window: PredictionThreshold
+    # stubs_enum.rs: the game compares (input, InputStatus) tuples, so Predicted vs Confirmed matters
+    (G.Game.STUB_ENUM, 2, 8, 1, 1, 0b01, False, (1, 4)),
+    (G.Game.STUB_ENUM, 2, 6, 0, 2, 0b10, True, (0, 5)),
 ]
 
 
@@ -242,7 +245,8 @@ def test_gpu_p2p_matches_oracle_every_tick(gpu_available, case):
     game, P, W, d, rd, mask, sparse, (lo, hi) = case
     S, T = 70, 90
     dt = np.uint32 if game == G.Game.STUB else np.uint8
-    inputs, upto, rin = synth_network(S, P, T, mask, rd, lo, hi, dtype=dt, mask=0x3 if game == G.Game.STUB else 0x0F)
+    imask = {G.Game.STUB: 0x3, G.Game.STUB_ENUM: 0x1}.get(game, 0x0F)
+    inputs, upto, rin = synth_network(S, P, T, mask, rd, lo, hi, dtype=dt, mask=imask)
     sess, orc = gpu_pair(game, S, P, W, d, rd, mask, sparse)
     di = torch.from_numpy(inputs).cuda()
     du = torch.from_numpy(upto).cuda()

@@ -65,6 +65,8 @@ def on_input_reference(last, start, data, ref_input, max_pred, ib):
         return {}, last, -2
     if last != -1 and start - 1 < last - 2 * max_pred:
         return {}, last, 1
+    if last != -1 and start - 1 < -1:  # recv_inputs holds no such frame: the packet is ignored (:653)
+        return {}, last, 1
     ref = bytes(ib) if (last == -1 or start - 1 == -1) else ref_input
     dec = O.wire_decode(ref, data)
     if dec is None:
@@ -127,6 +129,9 @@ def test_gpu_encode_matches_oracle_and_decode_matches_on_input(gpu_available, ib
         if lens[s] > 0:
             lens[s] = max(1, lens[s] - 1)
             pk_h2[s, lens[s] - 1] |= 0x80  # truncated varint / literal
+    neg = np.nonzero(~bad & (lens > 0))[0][:25]  # packets claiming a negative start frame
+    start[neg] = -3
+    last[neg] = np.minimum(last[neg], 4).clip(0)
     upto = np.full((P, S), -1, np.int32)
     upto[h] = last
     d_recv = torch.from_numpy(recv).cuda()
