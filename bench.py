@@ -504,23 +504,30 @@ def main():
     audit_bad = torch.zeros((), dtype=torch.int64, device=dev)  # DesyncDetected: owner vs replica checksums
     gathers = [0]
 
-    def run(t0, t1):
-        """Ticks [t0, t1): native multi-tick calls of at most --ticks-per-launch
+    def chunks(t0, t1):
+        """Ticks [t0, t1) as native multi-tick calls of at most --ticks-per-launch
         ticks (one steady_kernel launch each once past the first cd+1 ticks),
-        split further at desync-report points."""
-        t, steady_launches = t0, 0
+        split further at desync-report points: (input slice, steady, report after).
+        SyncTest's current frame after t ticks is t, so the split is known up
+        front and the slices are views made before the timed region."""
+        out, t = [], t0
         while t < t1:
             n = min(t1 - t, args.ticks_per_launch)
-            steady = sess.current_frame() > cd
+            steady = t > cd
             if not steady:  # start-up ticks: per-tick launches, then align the steady chunks
-                n = min(n, cd + 1 - sess.current_frame())
+                n = min(n, cd + 1 - t)
             if world > 1 and args.report_interval:
-                to_report = args.report_interval - sess.current_frame() % args.report_interval
-                n = min(n, to_report)
-            sess.run_ticks(dinputs[t:t + n])
-            steady_launches += steady
+                n = min(n, args.report_interval - t % args.report_interval)
             t += n
-            if world > 1 and args.report_interval and sess.current_frame() % args.report_interval == 0:
+            out.append((dinputs[t - n:t], steady, world > 1 and args.report_interval and t % args.report_interval == 0))
+        return out
+
+    def run(plan):
+        steady_launches = 0
+        for x, steady, report in plan:
+            sess.run_ticks(x)
+            steady_launches += steady
+            if report:
                 f = sess.current_frame() - 1
                 sess.export_checksum_report(f, reports.data_ptr())
                 gathered = shard.gather_reports(reports)  # RCCL all-gather of desync reports
@@ -529,8 +536,9 @@ def main():
                 gathers[0] += 1
         return steady_launches
 
+    timed_plan = chunks(warm, T)
     with torch.cuda.stream(stream):
-        run(0, warm)
+        run(chunks(0, warm))
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -538,7 +546,7 @@ def main():
         sess.profile_enable(True)
         sess.profile_take()
         t0 = time.perf_counter()
-        launches = run(warm, T)
+        launches = run(timed_plan)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()

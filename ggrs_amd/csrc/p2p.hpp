@@ -51,8 +51,7 @@ enum : int {
   QF_CONN_LAST = 5,    // ConnectionStatus::last_frame (messages.rs:5-18)
   QF_DISC = 6,         // ConnectionStatus::disconnected (0 / 1)
   QF_TAIL = 7,         // InputQueue: frame of inputs[tail] (input_queue.rs:83-101)
-  QF_LEN = 8,          // InputQueue::length
-  QF_COUNT = 9,
+  QF_COUNT = 8,
 };
 constexpr int kQsFields = QS_PLAYER0 + QF_COUNT * 4;
 // trace rows (the last tick of the last launch): LoadGameState frame, AdvanceFrame count, SaveGameState count
@@ -256,18 +255,24 @@ __device__ __forceinline__ int32_t group_min(int32_t v) {
 }
 
 // One InputQueue (input_queue.rs) in registers.  A frame is confirmed iff it is
-// <= last_added_frame; the tail (frame of inputs[tail]) and the length feed the
-// reference's `length <= INPUT_QUEUE_LENGTH` assert (:181), the one a caller
-// of the batch can trip: remote inputs delivered more than 128 frames past the
-// frames the session has discarded would overwrite ring entries still needed.
-// The inputs live in the HBM ring.
+// <= last_added_frame.  The tail (frame of inputs[tail]) feeds the reference's
+// `length <= INPUT_QUEUE_LENGTH` assert (:181), the one a caller of the batch
+// can trip: remote inputs delivered more than 128 frames past the frames the
+// session has discarded would overwrite ring entries still needed.  Every
+// queue's first input is frame 0 (the delay fill, :227-231) and inputs are
+// added in frame order, so length = last_added - tail + 1 for a connected
+// player (discard only resets it for a disconnected one, see q_discard): the
+// assert fires in a tick's poll iff the poll leaves that above 128.  The
+// inputs live in the HBM ring.
 struct DevQueue {
   int32_t last_added, pred_frame, first_inc, last_req, conn_last;
   uint32_t pred_val;
   bool disc;  // ConnectionStatus::disconnected: set between launches only (rb_p2p_disconnect_player)
-  int32_t tail, len;
-  bool overflow;  // the :181 assert fired (the session panics)
+  int32_t tail;
 };
+__device__ __forceinline__ bool q_overflow(const DevQueue& q) {
+  return !q.disc && q.last_added != kNullFrame && q.last_added - q.tail + 1 > kQueueLen;
+}
 
 template <int IB>
 struct RingIO {
@@ -313,9 +318,6 @@ constexpr size_t p2p_lds_bytes(int block) {
 template <class R>
 __device__ __forceinline__ void q_add_by_frame(DevQueue& q, const R& r, int h, unsigned s, int32_t f, uint32_t v) {
   r.put(f, h, s, v);
-  q.tail = q.len == 0 ? f : q.tail;  // the first entry ever sits at the tail
-  q.len += 1;
-  q.overflow |= q.len > kQueueLen;  // assert!(self.length <= INPUT_QUEUE_LENGTH)
   q.last_added = f;
   if (q.pred_frame != kNullFrame) {
     if (q.first_inc == kNullFrame && v != q.pred_val) q.first_inc = f;
@@ -334,16 +336,13 @@ __device__ __forceinline__ int32_t q_add(DevQueue& q, const R& r, int h, unsigne
   q_add_by_frame(q, r, h, s, f, v);
   return f;
 }
-// input_queue.rs:83-101 discard_confirmed_frames(frame)
+// input_queue.rs:83-101 discard_confirmed_frames(frame), for the tail.  The
+// "delete all but the most recent" branch only a disconnected remote reaches
+// (the confirmed frame skips it): it is never added to again, so its length
+// no longer matters.
 __device__ __forceinline__ void q_discard(DevQueue& q, int32_t frame) {
   if (q.last_req != kNullFrame) frame = min(frame, q.last_req);
-  if (frame >= q.last_added) {  // delete all but the most recent (only a disconnected remote gets here)
-    q.tail = q.last_added;
-    q.len = 1;
-  } else if (frame > q.tail) {
-    q.len -= frame - q.tail;
-    q.tail = frame;
-  }
+  if (frame < q.last_added && frame > q.tail) q.tail = frame;
 }
 // input_queue.rs:104-146 input(requested_frame)
 template <class R>
@@ -413,10 +412,8 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
       q[j].conn_last = *qrow(QF_CONN_LAST, h);
       q[j].disc = *qrow(QF_DISC, h) != 0;
       q[j].tail = *qrow(QF_TAIL, h);
-      q[j].len = *qrow(QF_LEN, h);
-      q[j].overflow = false;
     } else {  // padding lane of a 4-lane group (P = 3): no player
-      q[j] = DevQueue{kNullFrame, kNullFrame, kNullFrame, kNullFrame, INT32_MAX, 0u, false, kNullFrame, 0, false};
+      q[j] = DevQueue{kNullFrame, kNullFrame, kNullFrame, kNullFrame, INT32_MAX, 0u, false, 0};
     }
   }
   // disconnect_player between launches: P2PSession::disconnect_frame, consumed
@@ -707,14 +704,13 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
 #pragma unroll
       for (int k = 0; k < kPre; ++k) rv_n[j][k] = load_remote(j, f + k);
     }
-    {  // input_queue.rs:181 assert!(self.length <= INPUT_QUEUE_LENGTH) fired during the poll
+    {  // input_queue.rs:181 assert!(self.length <= INPUT_QUEUE_LENGTH) fired during the poll.  No
+      // branch here: the panic status is picked up by the panic check after the threshold decision
+      // (a branch at this point would make the waitcnt pass wait for the loads in flight).
       bool ovf = false;
 #pragma unroll
-      for (int j = 0; j < PPL; ++j) ovf |= q[j].overflow;
-      if (group_min<L>(ovf ? 0 : 1) == 0) {
-        status = kP2PStatusPanic;
-        break;
-      }
+      for (int j = 0; j < PPL; ++j) ovf |= q_overflow(q[j]);
+      status = group_min<L>(ovf ? 0 : 1) == 0 ? kP2PStatusPanic : status;
     }
     if constexpr (kDesync) {  // the cells check_checksum_send_interval will read, before this tick's saves
       int32_t confirmed = INT32_MAX;
@@ -811,7 +807,6 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     *qrow(QF_LAST_REQ, h) = q[j].last_req;
     *qrow(QF_CONN_LAST, h) = q[j].conn_last;
     *qrow(QF_TAIL, h) = q[j].tail;
-    *qrow(QF_LEN, h) = q[j].len;
   }
   if (lead) {
     p.qs[QS_CUR * Spad + s] = cur;
