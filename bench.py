@@ -151,11 +151,12 @@ def measured_copy_gbps(dev, nbytes=1 << 30, iters=10):
     return gbps
 
 
-def pmc_traffic(cfg_key):
-    """HBM bytes per steady-state tick (all sessions) from the committed rocprofv3
-    PMC summary of this exact configuration (profiles/*pmc*.json, written by
-    tools/pmc_summary.py: FETCH_SIZE x2 + WRITE_SIZE per the gfx950 correction
-    in MI355X_MICROARCH.md), or None."""
+def pmc_profile(cfg_key):
+    """The committed rocprofv3 PMC summary of this exact configuration
+    (profiles/*pmc*.json, written by tools/pmc_summary.py; the newest round's
+    file wins), or None.  Its hbm_bytes_per_tick is FETCH_SIZE x2 + WRITE_SIZE
+    per the gfx950 correction in MI355X_MICROARCH.md; its `issue` block holds
+    SQ_INSTS_VALU, the clock and the VALU issue-slot fraction."""
     import glob
     best = None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
@@ -164,8 +165,40 @@ def pmc_traffic(cfg_key):
         except Exception:
             continue
         if d.get("config_key") == cfg_key and d.get("hbm_bytes_per_tick"):
-            best = d["hbm_bytes_per_tick"]
+            best = dict(d, file=os.path.relpath(path, ROOT))
     return best
+
+
+def roofline_block(bytes_per_launch, avg_kernel_s, ticks_per_launch, launches, kernel, prof, model):
+    """The bench line's roofline object.  `achieved`/`frac` are the contract's:
+    algorithmic bytes per launch (`model` says which bytes) over the measured
+    average launch time, against the 8 TB/s spec peak.  Next to them, from the
+    committed PMC profile of the same configuration: the HBM bytes the counters
+    saw (`traffic`, `traffic_frac`), the VALU issue-slot fraction, and the
+    resource that actually limits the kernel (`limiter`)."""
+    achieved = bytes_per_launch / avg_kernel_s / 1e9
+    r = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+         "traffic": None, "algorithmic_bytes_per_launch": bytes_per_launch, "bytes_model": model,
+         "kernel_avg_us": avg_kernel_s * 1e6, "ticks_per_launch": ticks_per_launch, "launches_timed": launches,
+         "kernel": kernel}
+    if prof:
+        traffic = prof["hbm_bytes_per_tick"] * ticks_per_launch
+        r["traffic"] = traffic
+        r["traffic_frac"] = traffic / avg_kernel_s / 1e9 / HBM_PEAK_GBS
+        r["pmc_profile"] = prof["file"]
+        iss = prof.get("issue")
+        if iss:
+            r["valu"] = {k: iss[k] for k in ("valu_insts_per_wave", "valu_issue_frac", "issue_stall_frac",
+                                              "waves_per_simd", "clock_GHz_sq", "l2_hit") if k in iss}
+            if r["traffic_frac"] > 0.7:
+                r["limiter"] = "hbm bandwidth"
+            elif iss["valu_issue_frac"] > 0.7:
+                r["limiter"] = "valu issue"
+            else:
+                r["limiter"] = (f"dependency latency: {iss['waves_per_simd']:.1f} waves/SIMD, "
+                                f"{iss['valu_issue_frac']:.2f} of VALU issue slots, HBM traffic "
+                                f"{r['traffic_frac']:.2f} of peak")
+    return r
 
 
 def rehearsal(args):
@@ -349,12 +382,13 @@ def bench_p2p(args):
             # 16 branch states stored, per select: the selected cells read back
             bytes_rank += branch / world * (state + 2 + P) + S * args.steps * state * 17 + selects / world * state
         avg_kernel_s = kernel_ms / 1e3 / max(1, launches)
-        achieved = bytes_rank / max(1, launches) / avg_kernel_s / 1e9
-        traffic = None  # HBM bytes per launch from the committed PMC profile of this exact configuration
-        if not (args.fanout or args.wire or args.sparse_saving):
-            per_tick = pmc_traffic(f"p2p ex_game P={P} W={W} d={args.input_delay} rd={args.remote_delay} "
-                                   f"lag={lo},{hi} S={S}")
-            traffic = per_tick * args.steps / max(1, launches) if per_tick else None
+        cfg_key = (f"p2p ex_game P={P} W={W} d={args.input_delay} rd={args.remote_delay} lag={lo},{hi} S={S}"
+                   + (" sparse" if args.sparse_saving else "") + (" fanout" if args.fanout else "")
+                   + (" wire" if args.wire else ""))
+        roofline = roofline_block(bytes_rank / max(1, launches), avg_kernel_s, args.steps / max(1, launches), launches,
+                                  f"p2p_kernel<ExGame<{P},true>>" + (" + fanout_kernel (per tick)" if args.fanout
+                                                                     else " (fused P2P ticks)"),
+                                  pmc_profile(cfg_key), "algorithmic: cells loaded/saved, inputs, deliveries")
         line = {
             "metric": "P2P session-frames simulated/sec (node), rollback to the first mispredicted frame",
             "value": adv / elapsed, "unit": "session-frames/s", "n_gpus": world, "steps": args.steps,
@@ -376,11 +410,7 @@ def bench_p2p(args):
                                        if args.fanout else None),
                        "prediction_threshold_hits": thr, "panics": panics,
                        "parallelism": f"session-sharded x{world}"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel_avg_us": avg_kernel_s * 1e6,
-                         "ticks_per_launch": args.steps / max(1, launches), "launches_timed": launches,
-                         "kernel": f"p2p_kernel<ExGame<{P},true>>" + (" + fanout_kernel (per tick)" if args.fanout
-                                                                          else " (fused P2P ticks)")},
+            "roofline": roofline,
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:
@@ -575,11 +605,21 @@ def main():
         # word implicit); brawler 256 entities x 8 i32
         nw = 256 * 8 if brawler else 5 * P
         bpt = algorithmic_bytes_per_session_tick(P, cd, nw=nw, cs_bytes=2, in_bytes=1)
+        if brawler:
+            # HBM-required bytes: the LoadGameState of a tick re-reads the cell the same lanes
+            # saved one tick earlier (an L2 hit), so only the saves must reach HBM
+            bpt -= 4 * nw
+            model = "HBM-required: cd saves x 8 KiB + checksums + inputs (the load re-reads an L2-hot cell)"
+        else:
+            model = "algorithmic (SURVEY 8d): 1 load + cd saves x 40 B, checksums, inputs, status"
         bytes_per_launch = bpt * (S + A) * ticks_per_launch  # the kernel runs the audit replicas too
-        achieved = bytes_per_launch / avg_kernel_s / 1e9
         cfg_key = f"{args.game} P={P} cd={cd} W={args.max_prediction} d={args.input_delay} S={S}"
-        per_tick = pmc_traffic(cfg_key)
-        traffic = per_tick * ticks_per_launch if per_tick else None
+        roofline = roofline_block(bytes_per_launch, avg_kernel_s, ticks_per_launch, launches,
+                                  (f"steady_kernel<Brawler<{P}>,{cd}>" if brawler else
+                                   f"steady_kernel<ExGame<{P},true>,{cd}>") + " (fused steady-state ticks)",
+                                  pmc_profile(cfg_key), model)
+        roofline["algorithmic_bytes_per_session_tick"] = bpt
+        roofline["measured_copy_GBps"] = measured_copy_gbps(dev)
         line = {
             "metric": METRIC,
             "value": value,
@@ -614,22 +654,7 @@ def main():
                                     "audit_sessions_per_rank": A, "audit_compared": A * world * gathers[0],
                                     "audit_desynced": int(audit_bad.item())} if world > 1 else None),
             },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": traffic,
-                "algorithmic_bytes_per_launch": bytes_per_launch,
-                "algorithmic_bytes_per_session_tick": bpt,
-                "kernel_avg_us": avg_kernel_s * 1e6,
-                "ticks_per_launch": ticks_per_launch,
-                "launches_timed": launches,
-                "kernel": (f"steady_kernel<Brawler<{P}>,{cd}>" if brawler else f"steady_kernel<ExGame<{P},true>,{cd}>")
-                          + " (fused steady-state ticks)",
-                "measured_copy_GBps": measured_copy_gbps(dev),
-            },
+            "roofline": roofline,
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:

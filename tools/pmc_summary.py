@@ -69,7 +69,7 @@ def main():
                 v = vals[1:] if len(vals) > 1 else vals
                 ent[c] = sum(v) / len(v)
     # the dominant kernel: the fused steady / P2P kernel of the bench line
-    steady = [k for k in summary["kernels"] if "steady_kernel" in k or "p2p_kernel" in k]
+    steady = [k for k in summary["kernels"] if "steady_kernel" in k or "p2p_kernel" in k or "fanout_kernel" in k]
     if steady:
         k = max(steady, key=lambda n: summary["kernels"][n].get("total_ns", 0.0))
         e = summary["kernels"][k]
@@ -78,7 +78,33 @@ def main():
             b = (2 * e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024
             summary["hbm_bytes_per_launch"] = b
             summary["hbm_bytes_per_tick"] = b / tpl
+            # the speculative fan-out runs one p2p_kernel and one fanout_kernel per tick: a tick's
+            # traffic is both dispatches'
+            if "fanout_kernel" in k:
+                for o in steady:
+                    if "p2p_kernel" in o and "FETCH_SIZE" in summary["kernels"][o]:
+                        eo = summary["kernels"][o]
+                        summary["hbm_bytes_per_tick"] += (2 * eo["FETCH_SIZE"] + eo["WRITE_SIZE"]) * 1024 / tpl
+                        summary["tick_kernels"] = [k, o]
             summary["hbm_bytes_raw_per_launch"] = (e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024
+        # Issue side (MI355X_MICROARCH.md: 1,024 SIMDs, a wave64 VALU instruction occupies a SIMD-32
+        # for 2 cycles at full rate; SQ_BUSY_CYCLES sums the 32 shader engines' SQs, GRBM_GUI_ACTIVE
+        # the 8 XCDs).  valu_issue_frac = SQ_INSTS_VALU * 2 / (1024 * elapsed cycles): the share of
+        # VALU issue slots used, a lower bound (f64 and transcendental ops take more than 2 cycles).
+        if "SQ_INSTS_VALU" in e and e.get("SQ_BUSY_CYCLES") and e.get("avg_ns"):
+            cyc = e["SQ_BUSY_CYCLES"] / 32.0
+            summary["issue"] = {
+                "valu_insts_per_launch": e["SQ_INSTS_VALU"],
+                "valu_insts_per_wave": e["SQ_INSTS_VALU"] / max(1.0, e.get("SQ_WAVES", 1.0)),
+                "elapsed_cycles": cyc,
+                "clock_GHz_sq": cyc / e["avg_ns"],
+                "clock_GHz_grbm": (e["GRBM_GUI_ACTIVE"] / 8.0 / e["avg_ns"]) if e.get("GRBM_GUI_ACTIVE") else None,
+                "valu_issue_frac": e["SQ_INSTS_VALU"] * 2.0 / (1024.0 * cyc),
+                "issue_stall_frac": e.get("SQ_WAIT_INST_ANY", 0.0) / max(1.0, e.get("SQ_WAVE_CYCLES", 1.0)),
+                "waves_per_simd": e.get("SQ_WAVES", 0.0) / 1024.0,
+                "l2_hit": (e["TCC_HIT_sum"] / (e["TCC_HIT_sum"] + e["TCC_MISS_sum"]))
+                if e.get("TCC_HIT_sum") is not None and e.get("TCC_MISS_sum") is not None else None,
+            }
     out = os.path.join(prof, f"{tag}_pmc.json")
     with open(out, "w") as f:
         json.dump(summary, f, indent=1, sort_keys=True)
