@@ -36,6 +36,7 @@ RB_GAME_BRAWLER = 5
 RB_FLAG_CHECKED = 1
 RB_FLAG_LANE_PER_SESSION = 2
 RB_P2P_FLAG_FANOUT = 4
+RB_GAME_PLUGIN_BASE = 1000
 RB_P2P_REPORTS_PER_TAKE = 8
 RB_P2P_EVENTS_KEPT = 16
 
@@ -115,6 +116,7 @@ SIGNATURES = [
     ("rb_debug_speed_clamp", _I32, [_I32, _P, _P, _P, _P, ctypes.c_int64]),
     ("rb_profile_enable", _I32, [_P, _I32]),
     ("rb_profile_take", _I32, [_P, ctypes.POINTER(ctypes.c_double), _PI32]),
+    ("rb_register_game_plugin", _I32, [ctypes.c_char_p, _PI32]),
     ("rb_p2p_config_init", None, [ctypes.POINTER(RbP2PConfig)]),
     ("rb_p2p_create", _I32, [ctypes.POINTER(RbP2PConfig), ctypes.POINTER(_P)]),
     ("rb_p2p_destroy", None, [_P]),
@@ -127,6 +129,7 @@ SIGNATURES = [
     ("rb_p2p_read_cells", _I32, [_P, _P, _P, _P]),
     ("rb_p2p_read_live", _I32, [_P, _P]),
     ("rb_p2p_state_bytes", _I32, [_P]),
+    ("rb_p2p_input_bytes", _I32, [_P]),
     ("rb_p2p_counters", _I32, [_P, _P]),
     ("rb_p2p_totals", _I32, [_P, _P]),
     ("rb_p2p_take_checksum_reports", _I32, [_P, _P]),

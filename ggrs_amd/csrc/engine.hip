@@ -29,7 +29,32 @@
 #include <string>
 #include <vector>
 
+#include <dlfcn.h>
+
 #include "kernels.hpp"
+#include "../../include/ggrs_amd_game.hpp"
+
+// ---- game plugins (rb_register_game_plugin): dlopen'ed libraries built from
+// plugin.hip, each creating the GameOps of one user game.  Entries live for the
+// process (a batch may hold the plugin's GameOps and kernels).
+namespace rb {
+namespace {
+struct Plugin {
+  std::string path;
+  void* handle;
+  GameOps* (*make)(int32_t, int32_t);
+};
+std::mutex g_plugins_mu;
+std::vector<Plugin> g_plugins;
+}  // namespace
+
+std::unique_ptr<GameOps> make_plugin_ops(int game, int players) {
+  std::lock_guard<std::mutex> lk(g_plugins_mu);
+  const int k = game - RB_GAME_PLUGIN_BASE;
+  if (k < 0 || k >= static_cast<int>(g_plugins.size())) return nullptr;
+  return std::unique_ptr<GameOps>(g_plugins[static_cast<size_t>(k)].make(players, RB_PLUGIN_ABI));
+}
+}  // namespace rb
 
 namespace rb {
 __global__ void sincos_kernel(const float* __restrict__ x, float* __restrict__ so, float* __restrict__ co, int64_t n,
@@ -217,6 +242,27 @@ void words_of(const rb_batch* b, const std::vector<uint32_t>& planes, int s, uin
 }  // namespace
 
 extern "C" {
+
+rb_status rb_register_game_plugin(const char* path, int32_t* game_id) {
+  if (!path || !game_id) return fail(nullptr, RB_INVALID_REQUEST, "rb_register_game_plugin: null argument");
+  std::lock_guard<std::mutex> lk(g_plugins_mu);
+  for (size_t k = 0; k < g_plugins.size(); ++k)
+    if (g_plugins[k].path == path) {
+      *game_id = RB_GAME_PLUGIN_BASE + static_cast<int32_t>(k);
+      return RB_OK;
+    }
+  void* h = dlopen(path, RTLD_NOW | RTLD_LOCAL);
+  if (!h) return fail(nullptr, RB_INVALID_REQUEST, std::string("cannot load game plugin: ") + dlerror());
+  auto abi = reinterpret_cast<int32_t (*)()>(dlsym(h, "rb_plugin_abi"));
+  auto make = reinterpret_cast<GameOps* (*)(int32_t, int32_t)>(dlsym(h, "rb_plugin_make_ops"));
+  if (!abi || !make || abi() != RB_PLUGIN_ABI) {
+    dlclose(h);
+    return fail(nullptr, RB_INVALID_REQUEST, "not a game plugin of this engine (rb_plugin_abi / rb_plugin_make_ops)");
+  }
+  g_plugins.push_back(Plugin{path, h, make});
+  *game_id = RB_GAME_PLUGIN_BASE + static_cast<int32_t>(g_plugins.size() - 1);
+  return RB_OK;
+}
 
 void rb_config_init(rb_config* c) {
   std::memset(c, 0, sizeof(*c));

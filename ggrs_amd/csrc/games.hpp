@@ -571,4 +571,77 @@ struct StubRandomCsGame : StubGame {
   static U128 cs128(CS c) { return c; }
 };
 
+// ============================================================================
+// A user's game (include/ggrs_amd_game.hpp contract) adapted to the engine's
+// game interface: one lane per session, frame supplied by the cell tag, image
+// = le32 frame || le32 words.  Instantiated by ggrs_amd/csrc/plugin.hip into a
+// plugin library (rb_register_game_plugin).
+// ============================================================================
+template <int Bytes>
+struct PackedInRec {
+  using T = uint64_t;
+};
+template <>
+struct PackedInRec<1> {
+  using T = uint8_t;
+};
+template <>
+struct PackedInRec<2> {
+  using T = uint16_t;
+};
+template <>
+struct PackedInRec<3> {
+  using T = uint32_t;
+};
+template <>
+struct PackedInRec<4> {
+  using T = uint32_t;
+};
+
+template <class U>
+struct PluginGame {
+  static_assert(U::kPlayers >= 1 && U::kPlayers <= 4, "plugin games have 1..4 players");
+  static_assert(U::kInputBytes == 1 || U::kInputBytes == 2 || U::kInputBytes == 4, "Input is 1, 2 or 4 bytes");
+  static_assert(U::kPlayers * U::kInputBytes <= 8, "all players' inputs of a frame must pack into 8 bytes");
+  static_assert(U::kStateWords >= 1 && U::kStateWords <= 64, "1..64 state words");
+  static constexpr int kPlayers = U::kPlayers;
+  static constexpr int kLanes = 1;
+  static constexpr int NWL = U::kStateWords;
+  static constexpr int kInputBytes = U::kInputBytes;
+  static constexpr int kImageBytes = 4 + 4 * NWL;
+  static constexpr bool kDisplay = false;
+  static constexpr int kCanonWords = NWL;
+  static constexpr bool kHasRangePath = false;
+  static constexpr bool kHasPrep = false;
+  static constexpr bool kUsesStatus = true;
+  using InRec = typename PackedInRec<kPlayers * kInputBytes>::T;
+  using CS = typename U::Checksum;
+
+  static void init(uint32_t* w) { U::init(w); }
+  static void image(const uint32_t* w, int32_t frame, uint8_t* out) {
+    std::memcpy(out, &frame, 4);
+    std::memcpy(out + 4, w, 4 * NWL);
+  }
+  static void word_loc(int k, int* lane, int* word) {
+    *lane = 0;
+    *word = k;
+  }
+  __device__ static bool in_range(const uint32_t (&)[NWL]) { return false; }
+  template <bool = false>
+  __device__ static void advance(uint32_t (&w)[NWL], InRec rec, int, uint32_t status_bits, uint32_t*) {
+    uint32_t in[kPlayers];
+    uint8_t st[kPlayers];
+#pragma unroll
+    for (int p = 0; p < kPlayers; ++p) {
+      const uint64_t v = static_cast<uint64_t>(rec) >> (8 * kInputBytes * p);
+      in[p] = static_cast<uint32_t>(kInputBytes == 4 ? v & 0xffffffffull : v & ((1ull << (8 * kInputBytes)) - 1));
+      st[p] = static_cast<uint8_t>(((status_bits >> p) & 1u) ? 2u : ((status_bits >> (8 + p)) & 1u));
+    }
+    U::advance(w, in, st);
+  }
+  __device__ static CS checksum(const uint32_t (&w)[NWL], int32_t frame, int, const CsCtx&) {
+    return U::checksum(w, frame);
+  }
+};
+
 }  // namespace rb

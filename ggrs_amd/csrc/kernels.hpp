@@ -683,6 +683,8 @@ struct GameOpsT final : GameOps {
 std::unique_ptr<GameOps> make_exgame_ops(int players, bool lane_per_session);
 std::unique_ptr<GameOps> make_brawler_ops(int players);
 std::unique_ptr<GameOps> make_stub_ops(int game, int players);
+// a game registered with rb_register_game_plugin (engine.hip); nullptr if unknown
+std::unique_ptr<GameOps> make_plugin_ops(int game, int players);
 
 inline std::unique_ptr<GameOps> make_game(int game, int players, bool lane_per_session) {
   switch (game) {
@@ -691,7 +693,7 @@ inline std::unique_ptr<GameOps> make_game(int game, int players, bool lane_per_s
     case RB_GAME_STUB:
     case RB_GAME_STUB_ENUM:
     case RB_GAME_STUB_RANDOM_CS: return make_stub_ops(game, players);
-    default: return nullptr;
+    default: return game >= RB_GAME_PLUGIN_BASE ? make_plugin_ops(game, players) : nullptr;
   }
 }
 

@@ -190,8 +190,9 @@ rb_status rb_p2p_create(const rb_p2p_config* cfg, rb_p2p** out) {
   if (cfg->max_prediction > 64 || cfg->input_delay + cfg->max_prediction + 2 > kQueueLen)
     return pfail(nullptr, RB_INVALID_REQUEST, "max_prediction / input delay do not fit the 128-entry input queue");
   if (cfg->game != RB_GAME_EX_GAME && cfg->game != RB_GAME_STUB && cfg->game != RB_GAME_STUB_ENUM &&
-      cfg->game != RB_GAME_BRAWLER)
-    return pfail(nullptr, RB_INVALID_REQUEST, "P2P batches support ex_game, the stub games and the brawler");
+      cfg->game != RB_GAME_BRAWLER && cfg->game < RB_GAME_PLUGIN_BASE)
+    return pfail(nullptr, RB_INVALID_REQUEST,
+                 "P2P batches support ex_game, the stub games, the brawler and registered plugin games");
   auto ops = make_game(cfg->game, cfg->num_players, (cfg->flags & RB_FLAG_LANE_PER_SESSION) != 0);
   if (!ops) return pfail(nullptr, RB_INVALID_REQUEST, "unsupported game / num_players combination");
   const bool fanout = (cfg->flags & RB_P2P_FLAG_FANOUT) != 0;
@@ -325,6 +326,7 @@ rb_status rb_p2p_set_stream(rb_p2p* b, void* s) {
 }
 
 int32_t rb_p2p_state_bytes(const rb_p2p* b) { return b->ops->image_bytes; }
+int32_t rb_p2p_input_bytes(const rb_p2p* b) { return b->ops->input_bytes; }
 
 rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs, int64_t local_stride,
                            const int32_t* remote_upto, const void* remote_inputs, int32_t remote_frames) {

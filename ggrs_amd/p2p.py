@@ -17,7 +17,7 @@ import enum
 import numpy as np
 
 from . import _lib as L
-from .session import INPUT_DTYPE, DeviceError, InvalidRequest, Panic
+from .session import DeviceError, InvalidRequest, Panic, input_dtype
 from .synth import SEED, splitmix64
 
 
@@ -51,7 +51,7 @@ class P2PSession:
         self.local_mask = int(cfg.local_mask)
         self.desync_interval = int(cfg.desync_interval)
         self.state_bytes = lib.rb_p2p_state_bytes(handle)
-        self.input_dtype = INPUT_DTYPE[game]
+        self.input_dtype = input_dtype(game, lib.rb_p2p_input_bytes(handle))
         self._keep = []
 
     def close(self):

@@ -96,6 +96,20 @@ class Game(enum.IntEnum):
 
 INPUT_DTYPE = {Game.EX_GAME: np.uint8, Game.STUB: np.uint32, Game.STUB_ENUM: np.uint8,
                Game.STUB_RANDOM_CS: np.uint32, Game.BRAWLER: np.uint8}
+_DTYPE_OF_BYTES = {1: np.uint8, 2: np.uint16, 4: np.uint32}
+
+
+def game_of(game_id: int):
+    """Game for the built-in ids, the plain int for a registered plugin game."""
+    try:
+        return Game(game_id)
+    except ValueError:
+        return int(game_id)
+
+
+def input_dtype(game, input_bytes: int):
+    """numpy dtype of one Input of `game` (plugin games: by their Input size)."""
+    return INPUT_DTYPE.get(game) or _DTYPE_OF_BYTES[input_bytes]
 
 
 def _raise(lib, handle, status: int):
@@ -148,7 +162,8 @@ class RequestList:
 class SessionBuilder:
     """builder.rs:32-377, SyncTest subset, plus the batch size and device."""
 
-    def __init__(self, game: Game = Game.EX_GAME, num_sessions: int = 1, device: int = 0):
+    def __init__(self, game=Game.EX_GAME, num_sessions: int = 1, device: int = 0):
+        """game: a Game, or the id ggrs_amd.plugin.register_game_plugin returned."""
         self._cfg = L.RbConfig()
         L.load().rb_config_init(ctypes.byref(self._cfg))
         self._cfg.game = int(game)
@@ -282,14 +297,14 @@ class SessionBuilder:
         if st != L.RB_OK:
             msg = (lib.rb_p2p_last_error(None) or b"").decode()
             raise InvalidRequest(msg) if st == L.RB_INVALID_REQUEST else DeviceError(msg)
-        return P2PSession(lib, h, Game(pc.game), pc)
+        return P2PSession(lib, h, game_of(pc.game), pc)
 
     def start_synctest_session(self) -> "SyncTestSession":  # :342-354
         lib = L.load()
         h = ctypes.c_void_p()
         st = lib.rb_synctest_create(ctypes.byref(self._cfg), ctypes.byref(h))
         _raise(lib, None, st)
-        return SyncTestSession(lib, h, Game(self._cfg.game), self._cfg)
+        return SyncTestSession(lib, h, game_of(self._cfg.game), self._cfg)
 
 
 # --------------------------------------------------------------------------- session
@@ -307,7 +322,7 @@ class SyncTestSession:
         self.input_delay = int(cfg.input_delay)
         self.checked = bool(cfg.flags & L.RB_FLAG_CHECKED)
         self.state_bytes = lib.rb_state_bytes(handle)
-        self.input_dtype = INPUT_DTYPE[game]
+        self.input_dtype = input_dtype(game, lib.rb_input_bytes(handle))
         self._keep = []  # host arrays referenced by queued copies
 
     # -- lifetime

@@ -52,6 +52,16 @@ typedef enum rb_game {
                                  no reference game exists: defined in oracle/ggrs_oracle.hpp */
 } rb_game;
 
+/* Games compiled outside the engine (include/ggrs_amd_game.hpp: the `Config`
+ * trait + handle_requests of the user's game as device code, built into a
+ * plugin library by ggrs_amd/csrc/plugin.hip).  rb_register_game_plugin
+ * loads one and returns its game id (RB_GAME_PLUGIN_BASE + k), valid for
+ * rb_config.game and rb_p2p_config.game from then on.  Registering the same
+ * path twice returns the same id.  RB_INVALID_REQUEST: the library cannot be
+ * loaded, lacks the entry points or was built for another plugin ABI. */
+#define RB_GAME_PLUGIN_BASE 1000
+rb_status rb_register_game_plugin(const char* path, int32_t* game_id);
+
 /* GGRSRequest kinds (lib.rs:170-194) for rb_last_requests. */
 typedef enum rb_request_kind { RB_REQ_SAVE = 0, RB_REQ_LOAD = 1, RB_REQ_ADVANCE = 2 } rb_request_kind;
 
@@ -288,6 +298,7 @@ rb_status rb_p2p_read_cells(rb_p2p* b, int32_t* tags, void* images, uint64_t* ch
 /* The game state after the last advance, images [S][rb_p2p_state_bytes] (frame word = current frame). */
 rb_status rb_p2p_read_live(rb_p2p* b, void* images);
 int32_t rb_p2p_state_bytes(const rb_p2p* b);
+int32_t rb_p2p_input_bytes(const rb_p2p* b);
 /* Counters since create: [0] PredictionThreshold hits, [1] unexpected math paths, [2] panicked sessions. */
 rb_status rb_p2p_counters(rb_p2p* b, uint32_t* out3);
 /* Work the device executed since create: [0] AdvanceFrame, [1] SaveGameState,

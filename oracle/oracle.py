@@ -17,16 +17,22 @@ LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
 REF_TESTS = os.path.join(_HERE, "build", "ref_tests")
 
 EX_GAME, STUB, STUB_ENUM, STUB_RANDOM_CS, BRAWLER = 1, 2, 3, 4, 5
+PLUGIN = 100  # the include/ggrs_amd_game.hpp game compiled into an oracle plugin build
 KIND_PANIC = 99
-_lib = None
+_libs = {}
 
 
-def load():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise ImportError(f"{LIB_PATH} missing: run `make -C oracle`")
-        lib = ctypes.CDLL(LIB_PATH)
+def plugin_lib(name: str) -> str:
+    """Path of the oracle built with a plugin game (oracle/Makefile `plugin`, PLUGIN_NAME=name)."""
+    return os.path.join(_HERE, "build", f"liboracle_{name}.so")
+
+
+def load(path: str = LIB_PATH):
+    """The oracle library at `path` (the standard build, or a plugin build)."""
+    if path not in _libs:
+        if not os.path.exists(path):
+            raise ImportError(f"{path} missing: run `make -C oracle`")
+        lib = ctypes.CDLL(path)
         P, I32, U64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint64
         PI32 = ctypes.POINTER(ctypes.c_int32)
         sig = {
@@ -76,8 +82,8 @@ def load():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        _lib = lib
-    return _lib
+        _libs[path] = lib
+    return _libs[path]
 
 
 def _ptr(a: np.ndarray):
@@ -88,8 +94,8 @@ class OracleBatch:
     """S independent reference sessions of one game (TEST ONLY)."""
 
     def __init__(self, game: int, num_players: int, max_prediction: int, check_distance: int,
-                 input_delay: int, num_sessions: int, seed: int = 0):
-        lib = load()
+                 input_delay: int, num_sessions: int, seed: int = 0, lib_path: str = LIB_PATH):
+        lib = load(lib_path)
         self._lib = lib
         self._h = lib.orc_batch_create(game, num_players, max_prediction, check_distance, input_delay,
                                        num_sessions, seed)
@@ -97,7 +103,7 @@ class OracleBatch:
             raise ValueError(lib.orc_last_error().decode())
         self.game, self.P, self.W, self.S = game, num_players, max_prediction, num_sessions
         self.image_bytes = lib.orc_image_bytes(game, num_players)
-        self.input_dtype = np.uint32 if lib.orc_input_bytes(game) == 4 else np.uint8
+        self.input_dtype = {1: np.uint8, 2: np.uint16, 4: np.uint32}[lib.orc_input_bytes(game)]
 
     def close(self):
         if self._h:
@@ -163,8 +169,8 @@ class OracleP2P:
     advance()."""
 
     def __init__(self, game: int, num_players: int, max_prediction: int, input_delay: int, local_mask: int,
-                 num_sessions: int, sparse_saving: bool = False, remote_delay: int = 0):
-        lib = load()
+                 num_sessions: int, sparse_saving: bool = False, remote_delay: int = 0, lib_path: str = LIB_PATH):
+        lib = load(lib_path)
         self._lib = lib
         self._h = lib.orc_p2p_create(game, num_players, max_prediction, input_delay, local_mask,
                                      int(sparse_saving), remote_delay, num_sessions)
@@ -172,7 +178,7 @@ class OracleP2P:
             raise ValueError(lib.orc_last_error().decode())
         self.game, self.P, self.W, self.S = game, num_players, max_prediction, num_sessions
         self.image_bytes = lib.orc_image_bytes(game, num_players)
-        self.input_dtype = np.uint32 if lib.orc_input_bytes(game) == 4 else np.uint8
+        self.input_dtype = {1: np.uint8, 2: np.uint16, 4: np.uint32}[lib.orc_input_bytes(game)]
 
     def close(self):
         if self._h:

@@ -13,12 +13,16 @@
 #include <thread>
 
 #include "ggrs_oracle.hpp"
+#ifdef RB_PLUGIN_GAME  // oracle/Makefile `plugin`: the user's game header is -included
+#include "plugin_game.hpp"
+using PluginU = RB_PLUGIN_GAME;
+#endif
 
 using namespace orc;
 
 namespace {
 
-enum GameId : int32_t { EX_GAME = 1, STUB = 2, STUB_ENUM = 3, STUB_RANDOM_CS = 4, BRAWLER = 5 };
+enum GameId : int32_t { EX_GAME = 1, STUB = 2, STUB_ENUM = 3, STUB_RANDOM_CS = 4, BRAWLER = 5, PLUGIN = 100 };
 constexpr int32_t KIND_PANIC = 99;
 
 struct BatchBase {
@@ -48,6 +52,10 @@ inline std::vector<uint8_t> image_of(const stub::StateStubEnum& s) {
   return v;
 }
 inline std::vector<uint8_t> image_of(const brawler::State& s) { return brawler::image(s); }
+#ifdef RB_PLUGIN_GAME
+inline std::vector<uint8_t> image_of(const plugin::State<PluginU>& s) { return plugin::image(s); }
+inline void corrupt_state(plugin::State<PluginU>& st, int32_t k, uint32_t m) { st.w.at(static_cast<size_t>(k)) ^= m; }
+#endif
 inline uint64_t display_checksum(const exgame::Game& g, int32_t* f) { *f = g.last_checksum.first; return g.last_checksum.second; }
 template <class G>
 inline uint64_t display_checksum(const G&, int32_t* f) { *f = NULL_FRAME; return 0; }
@@ -465,10 +473,18 @@ thread_local std::string g_err;
 extern "C" {
 
 int32_t orc_image_bytes(int32_t game, int32_t num_players) {
+#ifdef RB_PLUGIN_GAME
+  if (game == PLUGIN) return 4 + 4 * PluginU::kStateWords;
+#endif
   if (game == BRAWLER) return 4 + brawler::N * 32;
   return game == EX_GAME ? 36 + 20 * num_players : 8;
 }
-int32_t orc_input_bytes(int32_t game) { return (game == STUB || game == STUB_RANDOM_CS) ? 4 : 1; }
+int32_t orc_input_bytes(int32_t game) {
+#ifdef RB_PLUGIN_GAME
+  if (game == PLUGIN) return PluginU::kInputBytes;
+#endif
+  return (game == STUB || game == STUB_RANDOM_CS) ? 4 : 1;
+}
 
 // Returns NULL on a builder error (message via orc_last_error).
 void* orc_batch_create(int32_t game, int32_t num_players, int32_t max_prediction, int32_t check_distance,
@@ -490,6 +506,12 @@ void* orc_batch_create(int32_t game, int32_t num_players, int32_t max_prediction
       case STUB_RANDOM_CS:
         return new Batch<stub::Config, stub::RandomChecksumGameStub>(
             b, num_sessions, [&](int32_t s) { return stub::RandomChecksumGameStub(seed ^ (uint64_t(s) * 0x9e37ULL)); });
+#ifdef RB_PLUGIN_GAME
+      case PLUGIN:
+        if (num_players != PluginU::kPlayers) { g_err = "num_players differs from the plugin game's"; return nullptr; }
+        return new Batch<plugin::Config<PluginU>, plugin::Game<PluginU>>(b, num_sessions,
+                                                                       [&](int32_t) { return plugin::Game<PluginU>(); });
+#endif
       default: g_err = "unknown game"; return nullptr;
     }
   } catch (const std::exception& ex) {
@@ -536,6 +558,13 @@ void* orc_p2p_create(int32_t game, int32_t num_players, int32_t max_prediction, 
         return new P2PBatch<stub::EnumConfig, stub::GameStubEnum>(num_players, max_prediction, input_delay, local_mask,
                                                                   sp, remote_delay, num_sessions,
                                                                   [&](int32_t) { return stub::GameStubEnum{}; });
+#ifdef RB_PLUGIN_GAME
+      case PLUGIN:
+        if (num_players != PluginU::kPlayers) { g_err = "num_players differs from the plugin game's"; return nullptr; }
+        return new P2PBatch<plugin::Config<PluginU>, plugin::Game<PluginU>>(
+            num_players, max_prediction, input_delay, local_mask, sp, remote_delay, num_sessions,
+            [&](int32_t) { return plugin::Game<PluginU>(); });
+#endif
       case BRAWLER:
         return new P2PBatch<brawler::Config, brawler::Game>(num_players, max_prediction, input_delay, local_mask, sp,
                                                             remote_delay, num_sessions,
