@@ -36,6 +36,7 @@ RB_GAME_BRAWLER = 5
 RB_FLAG_CHECKED = 1
 RB_FLAG_LANE_PER_SESSION = 2
 RB_P2P_FLAG_FANOUT = 4
+RB_P2P_FLAG_PEER_STATUS = 8
 RB_GAME_PLUGIN_BASE = 1000
 RB_P2P_REPORTS_PER_TAKE = 8
 RB_P2P_EVENTS_KEPT = 16
@@ -126,6 +127,7 @@ SIGNATURES = [
     ("rb_p2p_read_status", _I32, [_P, _P, _P, _P, _P]),
     ("rb_p2p_disconnect_player", _I32, [_P, _I32, _P]),
     ("rb_p2p_read_frames", _I32, [_P, _P, _P]),
+    ("rb_p2p_read_queues", _I32, [_P, _P]),
     ("rb_p2p_read_cells", _I32, [_P, _P, _P, _P]),
     ("rb_p2p_read_live", _I32, [_P, _P]),
     ("rb_p2p_state_bytes", _I32, [_P]),
@@ -136,6 +138,7 @@ SIGNATURES = [
     ("rb_p2p_receive_checksum_reports", _I32, [_P, _I32, _P, _I32]),
     ("rb_p2p_read_desync_events", _I32, [_P, _P, _P, _P, _P, _P]),
     ("rb_p2p_debug_corrupt", _I32, [_P, _I32, _I32, ctypes.c_uint32]),
+    ("rb_p2p_receive_peer_connect_status", _I32, [_P, _I32, _P, _P]),
     ("rb_p2p_profile_enable", _I32, [_P, _I32]),
     ("rb_p2p_profile_take", _I32, [_P, ctypes.POINTER(ctypes.c_double), _PI32]),
     ("rb_decode_input_packets", _I32, [_I32, _P, _I32, _I32, _I32, _I32, _I32, _P, ctypes.c_int64, _P, _P, _P, _I32,

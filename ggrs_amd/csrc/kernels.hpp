@@ -649,10 +649,10 @@ struct GameOpsT final : GameOps {
   hipError_t launch_p2p(const P2PParams& p, int block, hipStream_t st) const override {
     const int grid = (p.Spad * G::kLanes + block - 1) / block;
     const size_t lds = p2p_lds_bytes<G>(block);
-    if (p.ds.interval > 0) {  // desync detection on (rb_p2p_config.desync_interval)
+    if (p.ds.interval > 0 || p.peer.on) {  // desync detection / peers' connect-status reports on
       if (p.sparse)  // sparse saving and the fan-out exclude each other (rb_p2p_create)
         hipLaunchKernelGGL((p2p_kernel<G, false, true, true>), dim3(grid), dim3(block), lds, st, p);
-      else if (kFanout && p.spec_on)
+      else if (kFanout && p.spec_on && !p.peer.on)  // the fan-out assumes connected queues
         hipLaunchKernelGGL((p2p_kernel<G, kFanout, false, true>), dim3(grid), dim3(block), lds, st, p);
       else
         hipLaunchKernelGGL((p2p_kernel<G, false, false, true>), dim3(grid), dim3(block), lds, st, p);

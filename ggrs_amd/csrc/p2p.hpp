@@ -51,7 +51,8 @@ enum : int {
   QF_CONN_LAST = 5,    // ConnectionStatus::last_frame (messages.rs:5-18)
   QF_DISC = 6,         // ConnectionStatus::disconnected (0 / 1)
   QF_TAIL = 7,         // InputQueue: frame of inputs[tail] (input_queue.rs:83-101)
-  QF_COUNT = 8,
+  QF_LEN = 8,          // InputQueue::length
+  QF_COUNT = 9,
 };
 constexpr int kQsFields = QS_PLAYER0 + QF_COUNT * 4;
 // trace rows (the last tick of the last launch): LoadGameState frame, AdvanceFrame count, SaveGameState count
@@ -102,6 +103,16 @@ struct DesyncParams {
   int32_t interval;   // 0 = DesyncDetection::Off
 };
 
+// Peers' connect-status reports (UdpProtocol::peer_connect_status,
+// protocol.rs:158-160, 627-636) for update_player_disconnects
+// (p2p_session.rs:707-742): what the peer behind remote handle e last reported
+// about player i, merged by rb_p2p_receive_peer_connect_status.
+struct PeerParams {
+  int32_t* last;  // [4 endpoints][4 players][Spad] ConnectionStatus::last_frame
+  int32_t* disc;  // [4][4][Spad] ConnectionStatus::disconnected (0 / 1)
+  int32_t on;     // RB_P2P_FLAG_PEER_STATUS
+};
+
 struct P2PParams {
   uint32_t* snap;
   void* cs;
@@ -133,6 +144,7 @@ struct P2PParams {
   uint32_t local_mask;
   int32_t sparse;
   DesyncParams ds;
+  PeerParams peer;
 };
 
 // The cells as check_checksum_send_interval sees them.  It runs inside
@@ -254,25 +266,29 @@ __device__ __forceinline__ int32_t group_min(int32_t v) {
   return v;
 }
 
-// One InputQueue (input_queue.rs) in registers.  A frame is confirmed iff it is
-// <= last_added_frame.  The tail (frame of inputs[tail]) feeds the reference's
-// `length <= INPUT_QUEUE_LENGTH` assert (:181), the one a caller of the batch
-// can trip: remote inputs delivered more than 128 frames past the frames the
-// session has discarded would overwrite ring entries still needed.  Every
-// queue's first input is frame 0 (the delay fill, :227-231) and inputs are
-// added in frame order, so length = last_added - tail + 1 for a connected
-// player (discard only resets it for a disconnected one, see q_discard): the
-// assert fires in a tick's poll iff the poll leaves that above 128.  The
-// inputs live in the HBM ring.
+// One InputQueue (input_queue.rs) in registers; the inputs live in the ring
+// (HBM, or LDS inside a launch).  `tail` is the frame of inputs[tail] and
+// `len` the queue's length, restated exactly: every queue's first input is
+// frame 0 (the delay fill, :227-231) and inputs are added in frame order, so
+// ring slot k holds the newest frame <= last_added congruent to k mod 128 (or
+// none), which is all the reference's index arithmetic ever reads.  A frame is
+// Confirmed iff 0 <= f - tail < len (:118-127); for a connected player that is
+// f <= last_added.  `bad` records a reference assert / checked-arithmetic
+// panic inside a tick: input() below the tail (:113) and a discard that
+// would take `length` below zero (:99, a subtract-with-overflow panic in the
+// reference's test builds); the kernel folds it into the tick's status.
 struct DevQueue {
   int32_t last_added, pred_frame, first_inc, last_req, conn_last;
   uint32_t pred_val;
-  bool disc;  // ConnectionStatus::disconnected: set between launches only (rb_p2p_disconnect_player)
-  int32_t tail;
+  bool disc;  // ConnectionStatus::disconnected: rb_p2p_disconnect_player, or peers' reports (kNet)
+  bool bad;
+  int32_t tail, len;
 };
-__device__ __forceinline__ bool q_overflow(const DevQueue& q) {
-  return !q.disc && q.last_added != kNullFrame && q.last_added - q.tail + 1 > kQueueLen;
-}
+// input_queue.rs:181 assert!(self.length <= INPUT_QUEUE_LENGTH): a caller of
+// the batch trips it by delivering remote inputs more than 128 frames past the
+// frames the session has discarded.  length only grows in add_input_by_frame,
+// so after a poll it is above 128 iff the assert fired during the poll.
+__device__ __forceinline__ bool q_overflow(const DevQueue& q) { return q.len > kQueueLen; }
 
 template <int IB>
 struct RingIO {
@@ -319,6 +335,7 @@ template <class R>
 __device__ __forceinline__ void q_add_by_frame(DevQueue& q, const R& r, int h, unsigned s, int32_t f, uint32_t v) {
   r.put(f, h, s, v);
   q.last_added = f;
+  q.len += 1;
   if (q.pred_frame != kNullFrame) {
     if (q.first_inc == kNullFrame && v != q.pred_val) q.first_inc = f;
     if (q.pred_frame == q.last_req && q.first_inc == kNullFrame) q.pred_frame = kNullFrame;
@@ -336,20 +353,33 @@ __device__ __forceinline__ int32_t q_add(DevQueue& q, const R& r, int h, unsigne
   q_add_by_frame(q, r, h, s, f, v);
   return f;
 }
-// input_queue.rs:83-101 discard_confirmed_frames(frame), for the tail.  The
-// "delete all but the most recent" branch only a disconnected remote reaches
-// (the confirmed frame skips it): it is never added to again, so its length
-// no longer matters.
+// input_queue.rs:83-101 discard_confirmed_frames(frame).  "Delete all but the
+// most recent" sets tail = head, whose slot holds last_added - 127 (nothing, a
+// NULL frame, before 127 frames were added) and length 1; only a disconnected
+// player reaches it (the confirmed frame skips it), and from then on its
+// queue answers Predicted for the frames it still holds (:118-142).
 __device__ __forceinline__ void q_discard(DevQueue& q, int32_t frame) {
   if (q.last_req != kNullFrame) frame = min(frame, q.last_req);
-  if (frame < q.last_added && frame > q.tail) q.tail = frame;
+  if (frame >= q.last_added) {
+    q.tail = max(q.last_added - (kQueueLen - 1), kNullFrame);
+    q.len = 1;
+  } else if (frame > q.tail) {
+    const int32_t off = frame - q.tail;
+    q.bad |= off > q.len;  // `self.length -= offset` would underflow
+    q.len -= off;
+    // tail moves `off` slots: onto frame `frame`, except from a NULL head slot
+    // (fewer than 127 frames added), where slot last_added + 2 holds frame 0
+    // only if last_added == 126
+    q.tail = (q.tail == kNullFrame && q.last_added != kQueueLen - 2) ? kNullFrame : frame;
+  }
 }
 // input_queue.rs:104-146 input(requested_frame)
 template <class R>
 __device__ __forceinline__ uint32_t q_input(DevQueue& q, const R& r, int h, unsigned s, int32_t f) {
   q.last_req = f;
+  q.bad |= f < q.tail;  // assert!(requested_frame >= self.inputs[self.tail].frame) (:113)
   if (q.pred_frame < 0) {
-    if (q.last_added != kNullFrame && f <= q.last_added) return r.get(f, h, s);  // Confirmed
+    if (f - q.tail < q.len) return r.get(f, h, s);  // Confirmed (:118-127)
     if (f == 0 || q.last_added == kNullFrame) {
       q.pred_val = 0u;  // blank_input
       q.pred_frame = 0;  // NULL_FRAME + 1
@@ -361,10 +391,11 @@ __device__ __forceinline__ uint32_t q_input(DevQueue& q, const R& r, int h, unsi
   return q.pred_val;  // Predicted
 }
 
-// kSpec / kSparse / kDesync: the fan-out select, sparse saving and desync
-// detection are compiled in only where the batch uses them (fewer live
-// scalars: no SGPR spills on the plain path)
-template <class G, bool kSpec, bool kSparse, bool kDesync>
+// kSpec / kSparse / kNet: the fan-out select, sparse saving and the
+// network-fed bookkeeping (desync detection, peers' connect-status reports)
+// are compiled in only where the batch uses them (fewer live scalars: no SGPR
+// spills on the plain path)
+template <class G, bool kSpec, bool kSparse, bool kNet>
 __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
   using InRec = typename G::InRec;
   using CS = typename G::CS;
@@ -412,6 +443,8 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
       q[j].conn_last = *qrow(QF_CONN_LAST, h);
       q[j].disc = *qrow(QF_DISC, h) != 0;
       q[j].tail = *qrow(QF_TAIL, h);
+      q[j].len = *qrow(QF_LEN, h);
+      q[j].bad = false;
     } else {  // padding lane of a 4-lane group (P = 3): no player
       q[j] = DevQueue{kNullFrame, kNullFrame, kNullFrame, kNullFrame, INT32_MAX, 0u, false, 0};
     }
@@ -613,6 +646,12 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
 #pragma unroll
       for (int j = 0; j < PPL; ++j) q_discard(q[j], last_conf - 1);
     }
+    // an InputQueue panic in this tick's resimulation or discard (DevQueue::bad); the advance
+    // of the new frame cannot raise one (its frame is above every tail)
+    bool bad = false;
+#pragma unroll
+    for (int j = 0; j < PPL; ++j) bad |= q[j].bad;
+    status = group_min<L>(bad ? 0 : 1) == 0 ? kP2PStatusPanic : status;
   };
 
   // ---- the per-tick delivery tensors, loaded one tick ahead: at the top of
@@ -648,9 +687,10 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
   // the lead lane runs it, the group learns whether it panicked
   [[maybe_unused]] CellSnap send_cells{};
   auto run_desync = [&]() __attribute__((always_inline)) -> bool {
-    if constexpr (!kDesync) {
+    if constexpr (!kNet) {
       return true;
     } else {
+      if (p.ds.interval <= 0) return true;
       bool ok = true;
       if (lead) ok = desync_step(p.ds, send_cells, s, Spad, cur, last_saved, W, P, p.local_mask);
       return group_min<L>(ok ? 1 : 0) == 1;
@@ -712,12 +752,61 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
       for (int j = 0; j < PPL; ++j) ovf |= q_overflow(q[j]);
       status = group_min<L>(ovf ? 0 : 1) == 0 ? kP2PStatusPanic : status;
     }
-    if constexpr (kDesync) {  // the cells check_checksum_send_interval will read, before this tick's saves
-      int32_t confirmed = INT32_MAX;
+    if constexpr (kNet) {
+      // ---- update_player_disconnects (p2p_session.rs:274-275, 707-742), before the
+      // confirmed frame is taken.  Every lane of the group runs the handle loop on the
+      // gathered connection flags (the same values in every lane), then keeps its own
+      // handles' results.  Each remote handle is its own endpoint: an endpoint runs
+      // until its player is disconnected.
+      if (p.peer.on) {
+        bool dsc[P];
+        int32_t lastf[P];
 #pragma unroll
-      for (int j = 0; j < PPL; ++j) confirmed = min(confirmed, conn_of(j));
-      confirmed = group_min<L>(confirmed);  // confirmed_frame (:487-498)
-      if (lead && cur % p.ds.interval == 0) send_cells = snap_send_cells(csa, p.tag, s, Spad, W, cur, confirmed, last_saved);
+        for (int h = 0; h < P; ++h) {
+          if constexpr (kSplit) {
+            const int src = static_cast<int>(__lane_id()) - lane + h;
+            dsc[h] = __shfl(q[0].disc ? 1 : 0, src, 64) != 0;
+            lastf[h] = __shfl(q[0].conn_last, src, 64);
+          } else {
+            dsc[h] = q[h].disc;
+            lastf[h] = q[h].conn_last;
+          }
+        }
+        auto at = [&](int e, int i) { return (static_cast<size_t>(e) * 4 + static_cast<size_t>(i)) * Spad + s; };
+#pragma unroll
+        for (int h = 0; h < P; ++h) {
+          bool queue_connected = true;
+          int32_t queue_min = INT32_MAX;
+#pragma unroll
+          for (int e = 0; e < P; ++e) {
+            if (((p.local_mask >> e) & 1u) || dsc[e]) continue;  // !endpoint.is_running()
+            queue_connected = queue_connected && p.peer.disc[at(e, h)] == 0;
+            queue_min = min(queue_min, p.peer.last[at(e, h)]);
+          }
+          const bool local_connected = !dsc[h];
+          if (local_connected) queue_min = min(queue_min, lastf[h]);
+          if (!queue_connected && (local_connected || lastf[h] > queue_min) && !((p.local_mask >> h) & 1u)) {
+            dsc[h] = true;  // disconnect_player_at_frame(h, queue_min) (:555-581)
+            if (cur > queue_min) disc_frame = queue_min + 1;
+          }
+        }
+        any_disc = false;
+#pragma unroll
+        for (int j = 0; j < PPL; ++j) {
+          const int h = player_of(j);
+          if (h < P) q[j].disc = dsc[h];
+        }
+#pragma unroll
+        for (int h = 0; h < P; ++h) any_disc |= dsc[h];
+      }
+      // ---- the cells check_checksum_send_interval will read, before this tick's saves
+      if (p.ds.interval > 0) {
+        int32_t confirmed = INT32_MAX;
+#pragma unroll
+        for (int j = 0; j < PPL; ++j) confirmed = min(confirmed, conn_of(j));
+        confirmed = group_min<L>(confirmed);  // confirmed_frame (:487-498)
+        if (lead && cur % p.ds.interval == 0) send_cells = snap_send_cells(csa, p.tag, s, Spad, W, cur, confirmed, last_saved);
+      }
     }
     // ---- PredictionThreshold (sync_layer.rs:163-167) is decided by bookkeeping
     // alone: without sparse saving from the confirmed frame, with it by a dry run.
@@ -807,6 +896,8 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     *qrow(QF_LAST_REQ, h) = q[j].last_req;
     *qrow(QF_CONN_LAST, h) = q[j].conn_last;
     *qrow(QF_TAIL, h) = q[j].tail;
+    *qrow(QF_LEN, h) = q[j].len;
+    if constexpr (kNet) *qrow(QF_DISC, h) = q[j].disc ? 1 : 0;  // update_player_disconnects may set it
   }
   if (lead) {
     p.qs[QS_CUR * Spad + s] = cur;

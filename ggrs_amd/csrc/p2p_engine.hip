@@ -33,6 +33,7 @@ struct rb_p2p {
   std::vector<uint8_t> disconnected;  // host mirror [P][S] of ConnectionStatus::disconnected (validation)
   uint8_t* disc_mask = nullptr;       // [S] device copy of rb_p2p_disconnect_player's session mask
   DesyncParams ds{};                  // desync detection buffers (desync_interval > 0)
+  PeerParams peer{};                  // peers' connect-status reports (RB_P2P_FLAG_PEER_STATUS)
   bool prof = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev;
   size_t prof_used = 0;
@@ -66,6 +67,8 @@ void free_all(rb_p2p* b) {
                    b->ds.ev_frame, b->ds.ev_handle, b->ds.ev_local, b->ds.ev_remote};
   for (void* q : dptrs)
     if (q) (void)hipFree(q);
+  if (b->peer.last) (void)hipFree(b->peer.last);
+  if (b->peer.disc) (void)hipFree(b->peer.disc);
   for (auto& pr : b->prof_ev) {
     (void)hipEventDestroy(pr.first);
     (void)hipEventDestroy(pr.second);
@@ -144,6 +147,18 @@ __global__ void p2p_take_reports_kernel(DesyncParams d, rb_checksum_report* __re
     out[static_cast<size_t>(k) * S + s] = r;
   }
   d.ob_n[s] = 0;
+}
+
+// UdpProtocol::on_input's connect-status merge (protocol.rs:627-636) for one endpoint
+__global__ void p2p_peer_status_kernel(PeerParams pp, const int32_t* __restrict__ last, const uint8_t* __restrict__ disc,
+                                       int S, int Spad, int P, int e) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= S) return;
+  for (int i = 0; i < P; ++i) {
+    const size_t o = (static_cast<size_t>(e) * 4 + static_cast<size_t>(i)) * Spad + s;
+    pp.last[o] = max(pp.last[o], last[static_cast<size_t>(i) * S + s]);
+    pp.disc[o] = pp.disc[o] | (disc[static_cast<size_t>(i) * S + s] ? 1 : 0);
+  }
 }
 
 void image_from_planes(const rb_p2p* b, const std::vector<uint32_t>& planes, int s, int32_t frame, uint8_t* out) {
@@ -263,11 +278,19 @@ rb_status rb_p2p_create(const rb_p2p_config* cfg, rb_p2p** out) {
       qs[(QS_PLAYER0 + QF_PRED_VAL * 4 + h) * Sp + s] = 0;
       qs[(QS_PLAYER0 + QF_DISC * 4 + h) * Sp + s] = 0;  // ConnectionStatus::default: connected
       qs[(QS_PLAYER0 + QF_TAIL * 4 + h) * Sp + s] = 0;  // every queue's first input is frame 0
+      qs[(QS_PLAYER0 + QF_LEN * 4 + h) * Sp + s] = 0;
     }
   }
   b->disconnected.assign(static_cast<size_t>(b->P) * b->S, 0);
   P2P_CREATE(hipMalloc(&b->disc_mask, Sp));
   P2P_CREATE(hipMemcpyAsync(b->qs, qs.data(), qs.size() * 4, hipMemcpyHostToDevice, b->stream));
+  if (cfg->flags & RB_P2P_FLAG_PEER_STATUS) {  // ConnectionStatus::default for every (endpoint, player)
+    P2P_CREATE(hipMalloc(&b->peer.last, 16 * Sp * 4));
+    P2P_CREATE(hipMalloc(&b->peer.disc, 16 * Sp * 4));
+    P2P_CREATE(hipMemsetAsync(b->peer.last, 0xff, 16 * Sp * 4, b->stream));  // NULL_FRAME
+    P2P_CREATE(hipMemsetAsync(b->peer.disc, 0, 16 * Sp * 4, b->stream));
+    b->peer.on = 1;
+  }
   if (cfg->desync_interval > 0) {  // empty histories, outbox and event rings
     DesyncParams& d = b->ds;
     d.interval = cfg->desync_interval;
@@ -364,6 +387,7 @@ rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs,
   p.spec_cs = b->spec_cs;
   p.spec_meta = b->spec_meta;
   p.ds = b->ds;
+  p.peer = b->peer;
   FanParams fp{};
   fp.status = b->status;
   fp.snap = b->snap;
@@ -416,6 +440,14 @@ rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs,
 rb_status rb_p2p_disconnect_player(rb_p2p* b, int32_t handle, const uint8_t* session_mask) {
   if (handle < 0 || handle >= b->P) return pfail(b, RB_INVALID_REQUEST, "Invalid Player Handle.");
   if ((b->cfg.local_mask >> handle) & 1u) return pfail(b, RB_INVALID_REQUEST, "Local Player cannot be disconnected.");
+  if (b->peer.on) {  // peers' reports disconnect players inside the ticks: refresh the mirror
+    std::vector<int32_t> qs;
+    rb_status r = read_rows(b, b->qs, kQsFields, qs);
+    if (r != RB_OK) return r;
+    for (int h = 0; h < b->P; ++h)
+      for (int s = 0; s < b->S; ++s)
+        b->disconnected[static_cast<size_t>(h) * b->S + s] = qs[(QS_PLAYER0 + QF_DISC * 4 + h) * b->Spad + s] != 0;
+  }
   uint8_t* d = b->disconnected.data() + static_cast<size_t>(handle) * b->S;
   for (int s = 0; s < b->S; ++s)
     if ((!session_mask || session_mask[s]) && d[s]) return pfail(b, RB_INVALID_REQUEST, "Player already disconnected.");
@@ -456,6 +488,19 @@ rb_status rb_p2p_read_frames(rb_p2p* b, int32_t* current, int32_t* confirmed) {
     if (current) current[s] = qs[QS_CUR * b->Spad + s];
     if (confirmed) confirmed[s] = qs[QS_LAST_CONF * b->Spad + s];
   }
+  return RB_OK;
+}
+
+rb_status rb_p2p_read_queues(rb_p2p* b, int32_t* out) {
+  std::vector<int32_t> qs;
+  rb_status r = read_rows(b, b->qs, kQsFields, qs);
+  if (r != RB_OK) return r;
+  static constexpr int kField[RB_P2P_QUEUE_FIELDS] = {QF_LAST_ADDED, QF_TAIL, QF_LEN, QF_LAST_REQ,
+                                                      QF_PRED_FRAME, QF_FIRST_INC, QF_CONN_LAST, QF_DISC};
+  for (int s = 0; s < b->S; ++s)
+    for (int h = 0; h < b->P; ++h)
+      for (int k = 0; k < RB_P2P_QUEUE_FIELDS; ++k)
+        out[(static_cast<size_t>(s) * b->P + h) * RB_P2P_QUEUE_FIELDS + k] = qs[(QS_PLAYER0 + kField[k] * 4 + h) * b->Spad + s];
   return RB_OK;
 }
 
@@ -535,6 +580,19 @@ rb_status rb_p2p_receive_checksum_reports(rb_p2p* b, int32_t handle, const void*
   P2P_TRY(b, hipSetDevice(b->device));
   hipLaunchKernelGGL(p2p_receive_reports_kernel, dim3((b->S + 255) / 256), dim3(256), 0, b->stream, b->ds,
                      static_cast<const rb_checksum_report*>(dev_in), count, b->S, b->Spad, handle);
+  P2P_TRY(b, hipGetLastError());
+  return RB_OK;
+}
+
+rb_status rb_p2p_receive_peer_connect_status(rb_p2p* b, int32_t endpoint, const int32_t* last_frames,
+                                             const uint8_t* disconnected) {
+  if (!b->peer.on) return pfail(b, RB_INVALID_REQUEST, "peer connect status needs RB_P2P_FLAG_PEER_STATUS");
+  if (endpoint < 0 || endpoint >= b->P || ((b->cfg.local_mask >> endpoint) & 1u))
+    return pfail(b, RB_INVALID_REQUEST, "connect-status reports come from a remote handle's endpoint");
+  if (!last_frames || !disconnected) return pfail(b, RB_INVALID_REQUEST, "missing connect-status tensor");
+  P2P_TRY(b, hipSetDevice(b->device));
+  hipLaunchKernelGGL(p2p_peer_status_kernel, dim3((b->S + 255) / 256), dim3(256), 0, b->stream, b->peer, last_frames,
+                     disconnected, b->S, b->Spad, b->P, endpoint);
   P2P_TRY(b, hipGetLastError());
   return RB_OK;
 }

@@ -132,6 +132,14 @@ class P2PSession:
                                                  k.ctypes.data_as(ctypes.c_void_p)))
         return c, k
 
+    def read_queues(self):
+        """InputQueue / ConnectionStatus bookkeeping [S, P, 8]: last_added_frame, inputs[tail].frame,
+        length, last_requested_frame, prediction.frame, first_incorrect_frame, connect-status
+        last_frame, disconnected (input_queue.rs:12-34, messages.rs:5-18)."""
+        out = np.empty((self.num_sessions, self.num_players, 8), np.int32)
+        self._check(self._lib.rb_p2p_read_queues(self._h, out.ctypes.data_as(ctypes.c_void_p)))
+        return out
+
     def read_cells(self):
         """(frame tags [W, S], images [W, S, B], checksums [W, S, 2])."""
         W, S = self.max_prediction, self.num_sessions
@@ -198,6 +206,19 @@ class P2PSession:
         p = lambda a: a.ctypes.data_as(ctypes.c_void_p)
         self._check(self._lib.rb_p2p_read_desync_events(self._h, p(n), p(fr), p(hd), p(lo), p(ro)))
         return n, fr, hd, lo, ro
+
+    def receive_peer_connect_status(self, endpoint: int, last_frames, disconnected) -> None:
+        """The peer behind remote handle `endpoint` reports every player's ConnectionStatus
+        (UdpProtocol::on_input, protocol.rs:627-636): last_frames [P, S] int32 and
+        disconnected [P, S] uint8, CUDA tensors.  Needs with_peer_connect_status(True)."""
+        lp, lk = _dev_ptr(last_frames)
+        dp, dk = _dev_ptr(disconnected)
+        assert tuple(lk.shape) == (self.num_players, self.num_sessions) and tuple(dk.shape) == tuple(lk.shape)
+        self._keep = [lk, dk]
+        st = self._lib.rb_p2p_receive_peer_connect_status(self._h, int(endpoint), lp, dp)
+        if st == L.RB_INVALID_REQUEST:
+            raise InvalidRequest((self._lib.rb_p2p_last_error(self._h) or b"").decode())
+        self._check(st)
 
     def debug_corrupt(self, session: int, word: int, xor_mask: int) -> None:
         """Flip canonical state word `word` of the live state and every cell of `session`."""

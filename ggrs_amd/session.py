@@ -260,6 +260,12 @@ class SessionBuilder:
         self._desync = int(interval)
         return self
 
+    def with_peer_connect_status(self, on: bool) -> "SessionBuilder":
+        """P2P: track the peers' connect-status reports (P2PSession.receive_peer_connect_status)
+        and run update_player_disconnects (p2p_session.rs:707-742) every tick."""
+        self._peer_status = bool(on)
+        return self
+
     def with_remote_input_delay(self, delay: int) -> "SessionBuilder":
         """Frame of each remote handle's first input (the peers' input delay)."""
         self._remote_delay = int(delay)
@@ -289,7 +295,8 @@ class SessionBuilder:
         pc.remote_delay = getattr(self, "_remote_delay", 0)
         pc.sparse_saving = int(getattr(self, "_sparse", False))
         pc.flags = (self._cfg.flags & L.RB_FLAG_LANE_PER_SESSION) | (
-            L.RB_P2P_FLAG_FANOUT if getattr(self, "_fanout", False) else 0)
+            L.RB_P2P_FLAG_FANOUT if getattr(self, "_fanout", False) else 0) | (
+            L.RB_P2P_FLAG_PEER_STATUS if getattr(self, "_peer_status", False) else 0)
         pc.block_size = self._cfg.block_size
         pc.desync_interval = getattr(self, "_desync", 0)
         h = ctypes.c_void_p()

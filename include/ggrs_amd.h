@@ -249,6 +249,13 @@ typedef struct rb_p2p_config {
  * ex_game with one lane per player only; not with sparse saving. */
 #define RB_P2P_FLAG_FANOUT 4u
 
+/* Peers' connect-status reports (update_player_disconnects, p2p_session.rs:707-742):
+ * every advance_frame combines what the running endpoints last reported about
+ * each player (rb_p2p_receive_peer_connect_status) with the session's own
+ * view; a player some peer reports disconnected is disconnected here too, at
+ * the earliest reported frame, with the resimulation that implies. */
+#define RB_P2P_FLAG_PEER_STATUS 8u
+
 /* SessionBuilder::new() defaults for a 2-player session, handle 0 local, handle 1 remote. */
 void rb_p2p_config_init(rb_p2p_config* cfg);
 
@@ -293,6 +300,12 @@ rb_status rb_p2p_disconnect_player(rb_p2p* b, int32_t handle, const uint8_t* ses
 rb_status rb_p2p_read_status(rb_p2p* b, int32_t* status, int32_t* load_frame, int32_t* n_advance, int32_t* n_save);
 /* SyncLayer::current_frame and last_confirmed_frame per session.  Synchronises. */
 rb_status rb_p2p_read_frames(rb_p2p* b, int32_t* current, int32_t* confirmed);
+/* Every session's InputQueue / ConnectionStatus bookkeeping, out[S][P][RB_P2P_QUEUE_FIELDS]:
+ * last_added_frame, inputs[tail].frame, length, last_requested_frame, prediction.frame,
+ * first_incorrect_frame (input_queue.rs:12-34), ConnectionStatus::last_frame and
+ * disconnected (messages.rs:5-18).  For parity tests and debugging.  Synchronises. */
+#define RB_P2P_QUEUE_FIELDS 8
+rb_status rb_p2p_read_queues(rb_p2p* b, int32_t* out);
 /* All cells: frame tags [W][S], images [W][S][rb_p2p_state_bytes], checksums [W][S][2]. */
 rb_status rb_p2p_read_cells(rb_p2p* b, int32_t* tags, void* images, uint64_t* checksums);
 /* The game state after the last advance, images [S][rb_p2p_state_bytes] (frame word = current frame). */
@@ -338,6 +351,16 @@ rb_status rb_p2p_receive_checksum_reports(rb_p2p* b, int32_t handle, const void*
  * handle -1: none).  Any pointer may be NULL.  Synchronises. */
 rb_status rb_p2p_read_desync_events(rb_p2p* b, uint32_t* counts, int32_t* frames, int32_t* handles,
                                     uint64_t* local_checksums, uint64_t* remote_checksums);
+
+/* UdpProtocol::on_input's merge of the peer's connect status (protocol.rs:627-636)
+ * for the endpoint of remote handle `endpoint` in every session: the peer
+ * reports player i as last_frames[i * S + s] / disconnected[i * S + s] (device
+ * memory, [num_players][S] int32 and uint8); the stored status becomes
+ * (stored.disconnected || reported, max(stored.last_frame, reported)).
+ * Stream-ordered, between ticks.  RB_INVALID_REQUEST without
+ * RB_P2P_FLAG_PEER_STATUS or for a local handle. */
+rb_status rb_p2p_receive_peer_connect_status(rb_p2p* b, int32_t endpoint, const int32_t* last_frames,
+                                             const uint8_t* disconnected);
 
 /* Fault injection for tests (ex_game.rs:211-215 trigger_desync, generalised):
  * XOR `xor_mask` into canonical state word `word` of `session`'s live state

@@ -215,6 +215,8 @@ class InputQueue {
       // nothing to delete
     } else {
       size_t offset = static_cast<size_t>(frame - inputs[tail].frame);
+      // `self.length -= offset` (:99) is checked arithmetic in the reference's test builds
+      ORC_ASSERT(offset <= length);
       tail = (tail + offset) % INPUT_QUEUE_LENGTH;
       length -= offset;
     }
@@ -479,11 +481,13 @@ class SyncTestSession {
 // sessions/p2p_session.rs  P2PSession<T> — the rollback path without the
 // network layer.  UdpProtocol's job on this path is to turn packets into
 // Event::Input{input, player} in frame order (handle_event, :838-852); here the
-// caller delivers those inputs directly (deliver_remote_input).  Spectators,
-// time sync / wait recommendations, desync-report messages and the
-// synchronisation handshake (the session starts Running) are out of scope
-// (DESIGN.md §7).  disconnect_player (a user call between advance_frames) is
-// modelled; update_player_disconnects (peers' connect-status reports) is network.
+// caller delivers those inputs directly (deliver_remote_input), and likewise
+// the peers' ChecksumReports (on_checksum_report) and connect-status reports
+// (receive_peer_connect_status).  Spectators, time sync / wait
+// recommendations and the synchronisation handshake (the session starts
+// Running) are out of scope.  disconnect_player (a user call
+// between advance_frames), desync detection and update_player_disconnects
+// are modelled.
 // ---------------------------------------------------------------------------
 template <class C>
 class P2PSession {
@@ -517,11 +521,15 @@ class P2PSession {
     PlayerHandle handle;  // stands for `addr`: the remote endpoint
   };
   std::vector<DesyncEvent> events;
+  // UdpProtocol::peer_connect_status of each remote handle's endpoint (protocol.rs:158-160):
+  // what that peer last reported about every player's connection
+  std::vector<std::vector<ConnectionStatus>> peer_connect_status;
 
   // :160-213 (local players get the input delay; remote queues have none)
   P2PSession(size_t np, size_t mp, bool sparse, size_t delay, std::vector<bool> local)
       : num_players(np), max_prediction(mp), sparse_saving(sparse), sync_layer(np, mp),
-        local_connect_status(np), is_local(std::move(local)), remote_checksums(np) {
+        local_connect_status(np), is_local(std::move(local)), remote_checksums(np),
+        peer_connect_status(np, std::vector<ConnectionStatus>(np)) {
     for (size_t h = 0; h < np; ++h)
       if (is_local[h]) sync_layer.set_frame_delay(h, delay);
   }
@@ -566,10 +574,26 @@ class P2PSession {
     if (h >= num_players) return Error::invalid("Invalid Player Handle.");
     if (is_local[h]) return Error::invalid("Local Player cannot be disconnected.");
     if (local_connect_status[h].disconnected) return Error::invalid("Player already disconnected.");
-    Frame last_frame = local_connect_status[h].last_frame;
+    disconnect_player_at_frame(h, local_connect_status[h].last_frame);
+    return Error::ok();
+  }
+
+  // :555-595 disconnect_player_at_frame.  Each remote handle is its own
+  // endpoint here, so endpoint.disconnect() (the endpoint stops Running) is
+  // the handle's disconnected flag; a local handle is a no-op (:590).
+  void disconnect_player_at_frame(PlayerHandle h, Frame last_frame) {
+    if (is_local[h]) return;
     local_connect_status[h].disconnected = true;
     if (sync_layer.current_frame() > last_frame) disconnect_frame = last_frame + 1;
-    return Error::ok();
+  }
+
+  // UdpProtocol::on_input's merge of the peer's connect status (protocol.rs:627-636):
+  // the endpoint of remote handle `endpoint` reports player i as (disconnected, last_frame)
+  void receive_peer_connect_status(PlayerHandle endpoint, PlayerHandle i, bool disconnected, Frame last_frame) {
+    ORC_ASSERT(endpoint < num_players && !is_local[endpoint] && i < num_players);
+    auto& c = peer_connect_status[endpoint][i];
+    c.disconnected = disconnected || c.disconnected;
+    c.last_frame = std::max(c.last_frame, last_frame);
   }
 
   Frame confirmed_frame() const {  // :487-498
@@ -585,6 +609,7 @@ class P2PSession {
   Error advance_frame(std::vector<Request<C>>& requests) {
     requests.clear();
     if (sync_layer.current_frame() == 0) requests.push_back(sync_layer.save_current_state());
+    update_player_disconnects();  // :274-275
     Frame confirmed = confirmed_frame();
     Frame first_incorrect = sync_layer.check_simulation_consistency(disconnect_frame);
     if (first_incorrect != NULL_FRAME) {
@@ -621,6 +646,26 @@ class P2PSession {
   }
 
  private:
+  // :707-742.  An endpoint is Running until it is disconnected (the batch has
+  // no synchronising or timed-out endpoints: the session starts Running).
+  void update_player_disconnects() {
+    for (size_t handle = 0; handle < num_players; ++handle) {
+      bool queue_connected = true;
+      Frame queue_min_confirmed = INT32_MAX;
+      for (size_t e = 0; e < num_players; ++e) {  // player_reg.remotes.values()
+        if (is_local[e] || local_connect_status[e].disconnected) continue;  // !endpoint.is_running()
+        const ConnectionStatus& con = peer_connect_status[e][handle];
+        queue_connected = queue_connected && !con.disconnected;
+        queue_min_confirmed = std::min(queue_min_confirmed, con.last_frame);
+      }
+      const bool local_connected = !local_connect_status[handle].disconnected;
+      const Frame local_min_confirmed = local_connect_status[handle].last_frame;
+      if (local_connected) queue_min_confirmed = std::min(queue_min_confirmed, local_min_confirmed);
+      if (!queue_connected && (local_connected || local_min_confirmed > queue_min_confirmed))
+        disconnect_player_at_frame(handle, queue_min_confirmed);
+    }
+  }
+
   // :900-928.  The report is "sent" to every remote endpoint (sent_reports;
   // the caller forwards it to the peers' on_checksum_report).
   void check_checksum_send_interval() {

@@ -68,11 +68,13 @@ def load(path: str = LIB_PATH):
             "orc_p2p_read_cells": (I32, [P, P, P, P]),
             "orc_p2p_read_live": (I32, [P, P, P]),
             "orc_p2p_frames": (I32, [P, P, P]),
+            "orc_p2p_queues": (I32, [P, P]),
             "orc_p2p_set_desync": (None, [P, ctypes.c_uint32]),
             "orc_p2p_take_reports": (I32, [P, P, P, I32]),
             "orc_p2p_receive_reports": (I32, [P, I32, P, P, I32]),
             "orc_p2p_events": (I32, [P, P, P, P, P, P, I32]),
             "orc_p2p_corrupt": (I32, [P, I32, I32, ctypes.c_uint32]),
+            "orc_p2p_receive_peer_status": (I32, [P, I32, P, P]),
             "orc_wire_encode": (I32, [P, I32, P, I32, P, I32]),
             "orc_bench_p2p_exgame": (ctypes.c_double, [I32, I32, I32, ctypes.c_uint32, I32, I32, I32, I32, I32, P,
                                                         P, P, I32, P, P]),
@@ -242,6 +244,12 @@ class OracleP2P:
         self._lib.orc_p2p_frames(self._h, _ptr(c), _ptr(k))
         return c, k
 
+    def queues(self):
+        """InputQueue / ConnectionStatus bookkeeping [S, P, 8] (rb_p2p_read_queues's layout)."""
+        out = np.empty((self.S, self.P, 8), np.int32)
+        self._lib.orc_p2p_queues(self._h, _ptr(out))
+        return out
+
     # -- desync detection (p2p_session.rs:873-928)
     def set_desync_detection(self, interval: int) -> None:
         """DesyncDetection::On{interval} (0 = Off)."""
@@ -271,6 +279,13 @@ class OracleP2P:
         ro = np.empty((self.S, E), np.uint64)
         self._lib.orc_p2p_events(self._h, _ptr(n), _ptr(fr), _ptr(hd), _ptr(lo), _ptr(ro), E)
         return n, fr, hd, lo, ro
+
+    def receive_peer_connect_status(self, endpoint: int, last_frames, disconnected) -> None:
+        """The peer behind remote handle `endpoint` reports every player's
+        ConnectionStatus: last_frames [P, S] i32, disconnected [P, S] bool."""
+        lf = np.ascontiguousarray(np.broadcast_to(last_frames, (self.P, self.S)), np.int32)
+        dc = np.ascontiguousarray(np.broadcast_to(disconnected, (self.P, self.S)), np.uint8)
+        self._lib.orc_p2p_receive_peer_status(self._h, endpoint, _ptr(lf), _ptr(dc))
 
     def corrupt(self, session: int, word: int, xor_mask: int) -> None:
         """Flip canonical state word `word` of the live state and every saved cell."""

@@ -216,6 +216,7 @@ struct P2PBatchBase {
   virtual int32_t read_cells(int32_t* cell_frames, uint8_t* images, uint64_t* cs) = 0;
   virtual int32_t read_live(uint8_t* images, int32_t* frames) = 0;
   virtual int32_t frames(int32_t* current, int32_t* confirmed) = 0;
+  virtual int32_t queues(int32_t* out) = 0;  // [S][P][8], rb_p2p_read_queues's layout
   // desync detection (p2p_session.rs:873-928)
   virtual void set_desync(uint32_t interval) = 0;
   virtual int32_t take_reports(int32_t* frames, uint64_t* cs, int32_t K) = 0;
@@ -223,6 +224,7 @@ struct P2PBatchBase {
   virtual int32_t events(uint32_t* counts, int32_t* frames, int32_t* handles, uint64_t* local, uint64_t* remote,
                          int32_t E) = 0;
   virtual int32_t corrupt(int32_t session, int32_t word, uint32_t mask) = 0;
+  virtual int32_t receive_peer_status(int32_t endpoint, const int32_t* last_frames, const uint8_t* disconnected) = 0;
   std::string last_panic;
 };
 
@@ -388,6 +390,26 @@ struct P2PBatch : P2PBatchBase {
     return 0;
   }
 
+  int32_t queues(int32_t* out) override {
+    for (size_t s = 0; s < sess.size(); ++s) {
+      const auto& sl = sess[s]->sync_layer;
+      for (size_t h = 0; h < sl.input_queues.size(); ++h) {
+        const auto& q = sl.input_queues[h];
+        const auto& cs = sess[s]->local_connect_status[h];
+        int32_t* o = out + (s * sl.input_queues.size() + h) * 8;
+        o[0] = q.last_added_frame;
+        o[1] = q.inputs[q.tail].frame;
+        o[2] = static_cast<int32_t>(q.length);
+        o[3] = q.last_requested_frame;
+        o[4] = q.prediction.frame;
+        o[5] = q.first_incorrect_frame();
+        o[6] = cs.last_frame;
+        o[7] = cs.disconnected ? 1 : 0;
+      }
+    }
+    return 0;
+  }
+
   void set_desync(uint32_t interval) override {
     for (auto& ss : sess) ss->desync_interval = interval;
   }
@@ -447,6 +469,18 @@ struct P2PBatch : P2PBatchBase {
         if (local) local[o] = has ? static_cast<uint64_t>(ev[i].local_checksum) : 0;
         if (remote) remote[o] = has ? static_cast<uint64_t>(ev[i].remote_checksum) : 0;
       }
+    }
+    return 0;
+  }
+  // The peer behind remote handle `endpoint` reported every player's connection
+  // status: last_frames [P][S], disconnected [P][S] (UdpProtocol::on_input merge).
+  int32_t receive_peer_status(int32_t endpoint, const int32_t* last_frames, const uint8_t* disconnected) override {
+    const size_t S = sess.size();
+    for (size_t s = 0; s < S; ++s) {
+      if (panicked[s]) continue;
+      for (size_t i = 0; i < sess[s]->num_players; ++i)
+        sess[s]->receive_peer_connect_status(static_cast<PlayerHandle>(endpoint), i, disconnected[i * S + s] != 0,
+                                             last_frames[i * S + s]);
     }
     return 0;
   }
@@ -602,6 +636,7 @@ int32_t orc_p2p_read_live(void* b, uint8_t* images, int32_t* frames) {
 int32_t orc_p2p_frames(void* b, int32_t* current, int32_t* confirmed) {
   return static_cast<P2PBatchBase*>(b)->frames(current, confirmed);
 }
+int32_t orc_p2p_queues(void* b, int32_t* out) { return static_cast<P2PBatchBase*>(b)->queues(out); }
 void orc_p2p_set_desync(void* b, uint32_t interval) { static_cast<P2PBatchBase*>(b)->set_desync(interval); }
 int32_t orc_p2p_take_reports(void* b, int32_t* frames, uint64_t* cs, int32_t K) {
   return static_cast<P2PBatchBase*>(b)->take_reports(frames, cs, K);
@@ -615,6 +650,9 @@ int32_t orc_p2p_events(void* b, uint32_t* counts, int32_t* frames, int32_t* hand
 }
 int32_t orc_p2p_corrupt(void* b, int32_t session, int32_t word, uint32_t mask) {
   return static_cast<P2PBatchBase*>(b)->corrupt(session, word, mask);
+}
+int32_t orc_p2p_receive_peer_status(void* b, int32_t endpoint, const int32_t* last_frames, const uint8_t* disc) {
+  return static_cast<P2PBatchBase*>(b)->receive_peer_status(endpoint, last_frames, disc);
 }
 
 // network/compression.rs wire format (ggrs_oracle.hpp namespace wire).

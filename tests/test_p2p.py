@@ -220,6 +220,17 @@ def compare_state(sess, orc, tick, alive=None):
     oc, ok = orc.frames()
     np.testing.assert_array_equal(c[a], oc[a])
     np.testing.assert_array_equal(k[a], ok[a])
+    compare_queues(sess, orc, tick, a)
+
+
+def compare_queues(sess, orc, tick, alive):
+    """Every InputQueue's bookkeeping (last added / tail / length / last requested / prediction /
+    first incorrect frame) and ConnectionStatus == the oracle's."""
+    dq, oq = sess.read_queues(), orc.queues()
+    # inputs[tail].frame before a queue's first add: NULL in the reference, 0 on the device (the
+    # frame its first add puts there); nothing reads it before then
+    dq[:, :, 1] = np.where(dq[:, :, 0] < 0, oq[:, :, 1], dq[:, :, 1])
+    np.testing.assert_array_equal(dq[alive], oq[alive], err_msg=f"input queues, tick {tick}")
 
 
 CASES = [  # game, P, W, d, rd, local_mask, sparse, lag range

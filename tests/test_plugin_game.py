@@ -32,7 +32,8 @@ def orbit_inputs(S, T, seed=7):
 
 def test_plugin_library_exports_the_contract():
     lib = ctypes.CDLL(PLUGIN)
-    assert lib.rb_plugin_abi() == 2  # RB_PLUGIN_ABI in include/ggrs_amd_game.hpp
+    abi = int(open(os.path.join(ROOT, "include", "ggrs_amd_game.hpp")).read().split("#define RB_PLUGIN_ABI ")[1].split()[0])
+    assert lib.rb_plugin_abi() == abi  # the engine and the plugin agree on the kernel parameter layouts
     assert lib.rb_plugin_players() == P
     assert hasattr(lib, "rb_plugin_make_ops")
 
