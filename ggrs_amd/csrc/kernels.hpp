@@ -646,25 +646,35 @@ struct GameOpsT final : GameOps {
                        reinterpret_cast<rb_checksum_report*>(out));
     return hipGetLastError();
   }
+  template <bool kSpec, bool kSparse, bool kNet>
+  static hipError_t launch_p2p_as(const P2PParams& p, int grid, int block, hipStream_t st) {
+    size_t lds = p2p_lds_bytes<G>(block);
+    if constexpr (!kSpec && !kNet && p2p_lds_queue<G>()) {
+      if (p2p_lds_cells<G>(p.W)) {  // the snapshot ring in LDS (p2p_lds_cell_bytes)
+        auto k = p2p_kernel<G, kSpec, kSparse, kNet, true>;
+        lds += p2p_lds_cell_bytes<G>(block, p.W);
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           static_cast<int>(lds));
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k, dim3(grid), dim3(block), lds, st, p);
+        return hipGetLastError();
+      }
+    }
+    hipLaunchKernelGGL((p2p_kernel<G, kSpec, kSparse, kNet, false>), dim3(grid), dim3(block), lds, st, p);
+    return hipGetLastError();
+  }
   hipError_t launch_p2p(const P2PParams& p, int block, hipStream_t st) const override {
     const int grid = (p.Spad * G::kLanes + block - 1) / block;
-    const size_t lds = p2p_lds_bytes<G>(block);
     if (p.ds.interval > 0 || p.peer.on) {  // desync detection / peers' connect-status reports on
       if (p.sparse)  // sparse saving and the fan-out exclude each other (rb_p2p_create)
-        hipLaunchKernelGGL((p2p_kernel<G, false, true, true>), dim3(grid), dim3(block), lds, st, p);
-      else if (kFanout && p.spec_on && !p.peer.on)  // the fan-out assumes connected queues
-        hipLaunchKernelGGL((p2p_kernel<G, kFanout, false, true>), dim3(grid), dim3(block), lds, st, p);
-      else
-        hipLaunchKernelGGL((p2p_kernel<G, false, false, true>), dim3(grid), dim3(block), lds, st, p);
-    } else {
-      if (p.sparse)
-        hipLaunchKernelGGL((p2p_kernel<G, false, true, false>), dim3(grid), dim3(block), lds, st, p);
-      else if (kFanout && p.spec_on)
-        hipLaunchKernelGGL((p2p_kernel<G, kFanout, false, false>), dim3(grid), dim3(block), lds, st, p);
-      else
-        hipLaunchKernelGGL((p2p_kernel<G, false, false, false>), dim3(grid), dim3(block), lds, st, p);
+        return launch_p2p_as<false, true, true>(p, grid, block, st);
+      if (kFanout && p.spec_on && !p.peer.on)  // the fan-out assumes connected queues
+        return launch_p2p_as<kFanout, false, true>(p, grid, block, st);
+      return launch_p2p_as<false, false, true>(p, grid, block, st);
     }
-    return hipGetLastError();
+    if (p.sparse) return launch_p2p_as<false, true, false>(p, grid, block, st);
+    if (kFanout && p.spec_on) return launch_p2p_as<kFanout, false, false>(p, grid, block, st);
+    return launch_p2p_as<false, false, false>(p, grid, block, st);
   }
   static constexpr bool kFanout = G::kLanes > 1 && G::kLanes <= 4;
   hipError_t launch_fanout(const FanParams& p, int block, hipStream_t st) const override {

@@ -329,6 +329,26 @@ template <class G>
 constexpr size_t p2p_lds_bytes(int block) {
   return p2p_lds_queue<G>() ? static_cast<size_t>(kQueueLen) * static_cast<size_t>(block) : 0;
 }
+// The snapshot ring in LDS (p2p_kernel kLdsC): for the launch, the W cells
+// (words [W][NWL][block], frame tags and checksums [W][block / kLanes]) live
+// after the queue in LDS; the launch loads them from HBM first and writes
+// them back last.  Every SaveGameState and LoadGameState inside is an LDS
+// access, and the tick loop issues no global store at all: CDNA's vmcnt
+// retires loads and stores in issue order, so with a tick's snapshot stores
+// in flight, waiting for the next tick's prefetched deliveries would wait for
+// the stores too (the compiler cannot count stores issued in a loop of
+// data-dependent length and drains the counter).  Up to kLdsCellsMaxW cells:
+// at W = 8, 512 threads per CU (two waves per SIMD) take 156 KiB of the 160.
+constexpr int kLdsCellsMaxW = 8;
+template <class G>
+constexpr size_t p2p_lds_cell_bytes(int block, int W) {
+  return static_cast<size_t>(W) * (static_cast<size_t>(G::NWL) * 4 * block +
+                                   (4 + sizeof(typename G::CS)) * static_cast<size_t>(block / G::kLanes));
+}
+template <class G>
+constexpr bool p2p_lds_cells(int W) {
+  return p2p_lds_queue<G>() && W <= kLdsCellsMaxW;
+}
 
 // input_queue.rs:167-204 add_input_by_frame
 template <class R>
@@ -348,8 +368,10 @@ template <class R>
 __device__ __forceinline__ int32_t q_add(DevQueue& q, const R& r, int h, unsigned s, int32_t f, uint32_t v) {
   int32_t expected = q.last_added == kNullFrame ? 0 : q.last_added + 1;
   if (expected > f) return kNullFrame;
-  const uint32_t rep = q.last_added == kNullFrame ? 0u : r.get(q.last_added, h, s);
-  for (; expected < f; ++expected) q_add_by_frame(q, r, h, s, expected, rep);
+  if (expected < f) {  // only a queue's first add replicates (the input-delay fill)
+    const uint32_t rep = q.last_added == kNullFrame ? 0u : r.get(q.last_added, h, s);
+    for (; expected < f; ++expected) q_add_by_frame(q, r, h, s, expected, rep);
+  }
   q_add_by_frame(q, r, h, s, f, v);
   return f;
 }
@@ -395,7 +417,12 @@ __device__ __forceinline__ uint32_t q_input(DevQueue& q, const R& r, int h, unsi
 // network-fed bookkeeping (desync detection, peers' connect-status reports)
 // are compiled in only where the batch uses them (fewer live scalars: no SGPR
 // spills on the plain path)
-template <class G, bool kSpec, bool kSparse, bool kNet>
+// Attribution builds (tools/mkvar.sh -DRB_P2P_EXP=...): 1 drops the game's
+// AdvanceFrame math, 2 its save checksum.  Always 0 in the product.
+#ifndef RB_P2P_EXP
+#define RB_P2P_EXP 0
+#endif
+template <class G, bool kSpec, bool kSparse, bool kNet, bool kLdsC>
 __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
   using InRec = typename G::InRec;
   using CS = typename G::CS;
@@ -424,6 +451,12 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     if constexpr (kLdsQ) return LdsRing{lds_queue + threadIdx.x, blockDim.x};
     else return hbm;
   }();
+  static_assert(!kLdsC || (kLdsQ && !kSpec && !kNet),
+                "the LDS snapshot ring needs the LDS queue; the fan-out and desync detection read HBM cells mid-launch");
+  const unsigned bd = blockDim.x, tid = threadIdx.x, sl = tid / L, bps = bd / L;
+  uint32_t* const lds_cell = reinterpret_cast<uint32_t*>(lds_queue + kQueueLen * bd);  // [W][NW][bd]
+  int32_t* const lds_tag = reinterpret_cast<int32_t*>(lds_cell + static_cast<unsigned>(W) * NW * bd);  // [W][bps]
+  CS* const lds_cs = reinterpret_cast<CS*>(lds_tag + static_cast<unsigned>(W) * bps);  // [W][bps]
   auto qrow = [&](int field, int h) __attribute__((always_inline)) { return p.qs + static_cast<size_t>(QS_PLAYER0 + field * 4 + h) * Spad + s; };
   auto player_of = [&](int j) __attribute__((always_inline)) { return kSplit ? lane : j; };
 
@@ -480,6 +513,25 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     }
   }
 
+  if constexpr (kLdsC) {  // the snapshot ring of this launch's sessions into LDS
+#pragma unroll
+    for (int k = 0; k < kLdsCellsMaxW; ++k) {
+      const unsigned kk = static_cast<unsigned>(min(k, W - 1));
+      uint32_t cw[NW];
+      load_words<NW>(p.snap + kk * slot_words, static_cast<int>(Gpad), static_cast<int>(g), cw);
+      const int32_t tg = p.tag[kk * Spad + s];
+      const CS cv = csa[kk * Spad + s];
+      if (k < W) {
+#pragma unroll
+        for (int n = 0; n < NW; ++n) lds_cell[(kk * NW + n) * bd + tid] = cw[n];
+        if (lead) {
+          lds_tag[kk * bps + sl] = tg;
+          lds_cs[kk * bps + sl] = cv;
+        }
+      }
+    }
+  }
+
   int32_t status = kP2PStatusOk, load_frame = kNullFrame, nadv = 0, nsave = 0;
   uint32_t nonce = 0;
   uint32_t tot_adv = 0, tot_save = 0, tot_load = 0, tot_sel = 0;  // requests the game executed in this launch
@@ -496,12 +548,22 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     if (!exec) return;
     ++tot_save;
     CsCtx ctx{0ull, s, nonce++};
-    const CS c = G::checksum(w, f, lane, ctx);
+    CS c{};
+    if constexpr (!(RB_P2P_EXP & 2)) c = G::checksum(w, f, lane, ctx);
     const unsigned slot = static_cast<unsigned>(f % W);
-    store_words<NW>(p.snap + slot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), w);
-    if (lead) {
-      csa[slot * Spad + s] = c;
-      p.tag[slot * Spad + s] = f;
+    if constexpr (kLdsC) {
+#pragma unroll
+      for (int n = 0; n < NW; ++n) lds_cell[(slot * NW + n) * bd + tid] = w[n];
+      if (lead) {
+        lds_cs[slot * bps + sl] = c;
+        lds_tag[slot * bps + sl] = f;
+      }
+    } else {
+      store_words<NW>(p.snap + slot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), w);
+      if (lead) {
+        csa[slot * Spad + s] = c;
+        p.tag[slot * Spad + s] = f;
+      }
     }
   };
   // SyncLayer::synchronized_inputs (sync_layer.rs:187-200) for this lane's
@@ -527,7 +589,8 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     const InRec rec = sync_inputs(f, dmask);
     ++nadv;
     if (exec) {
-      G::advance(w, rec, lane, dmask, &p.counters[1]);
+      if constexpr (RB_P2P_EXP & 1) w[0] += static_cast<uint32_t>(rec);  // attribution builds only
+      else G::advance(w, rec, lane, dmask, &p.counters[1]);
       ++tot_adv;
     }
   };
@@ -536,12 +599,18 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     const int32_t to_load = kSparse ? last_saved : first_incorrect;
     const int32_t count = cur - to_load;
     const unsigned slot = static_cast<unsigned>(to_load % W);
-    if (to_load < 0 || to_load > first_incorrect || count <= 0 || count > W || p.tag[slot * Spad + s] != to_load) {
+    const int32_t tag = kLdsC ? lds_tag[slot * bps + sl] : p.tag[slot * Spad + s];
+    if (to_load < 0 || to_load > first_incorrect || count <= 0 || count > W || tag != to_load) {
       status = kP2PStatusPanic;  // a reference assert (sync_layer.rs:141-148) would fire
       return;
     }
     if (exec) {  // LoadGameState
-      load_words<NW>(p.snap + slot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), w);
+      if constexpr (kLdsC) {
+#pragma unroll
+        for (int n = 0; n < NW; ++n) w[n] = lds_cell[(slot * NW + n) * bd + tid];
+      } else {
+        load_words<NW>(p.snap + slot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), w);
+      }
       ++tot_load;
     }
     load_frame = to_load;
@@ -647,11 +716,16 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
       for (int j = 0; j < PPL; ++j) q_discard(q[j], last_conf - 1);
     }
     // an InputQueue panic in this tick's resimulation or discard (DevQueue::bad); the advance
-    // of the new frame cannot raise one (its frame is above every tail)
-    bool bad = false;
+    // of the new frame cannot raise one (its frame is above every tail).  Only peers' reports
+    // reach those states: without them a queue's tail never passes a frame a rollback reads
+    // (rollbacks start above the discarded frames) and only a disconnected player's queue
+    // takes the delete-all branch, after which it is read only past its last frame.
+    if constexpr (kNet) {
+      bool bad = false;
 #pragma unroll
-    for (int j = 0; j < PPL; ++j) bad |= q[j].bad;
-    status = group_min<L>(bad ? 0 : 1) == 0 ? kP2PStatusPanic : status;
+      for (int j = 0; j < PPL; ++j) bad |= q[j].bad;
+      status = group_min<L>(bad ? 0 : 1) == 0 ? kP2PStatusPanic : status;
+    }
   };
 
   // ---- the per-tick delivery tensors, loaded one tick ahead: at the top of
@@ -884,6 +958,19 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     }
   }
   // ---- write back
+  if constexpr (kLdsC) {  // the snapshot ring
+    for (int k = 0; k < W; ++k) {
+      const unsigned kk = static_cast<unsigned>(k);
+      uint32_t cw[NW];
+#pragma unroll
+      for (int n = 0; n < NW; ++n) cw[n] = lds_cell[(kk * NW + n) * bd + tid];
+      store_words<NW>(p.snap + kk * slot_words, static_cast<int>(Gpad), static_cast<int>(g), cw);
+      if (lead) {
+        csa[kk * Spad + s] = lds_cs[kk * bps + sl];
+        p.tag[kk * Spad + s] = lds_tag[kk * bps + sl];
+      }
+    }
+  }
   store_words<NW>(p.live, static_cast<int>(Gpad), static_cast<int>(g), w);
 #pragma unroll
   for (int j = 0; j < PPL; ++j) {
