@@ -189,13 +189,14 @@ def roofline_block(bytes_per_launch, avg_kernel_s, ticks_per_launch, launches, k
         iss = prof.get("issue")
         if iss:
             r["valu"] = {k: iss[k] for k in ("valu_insts_per_wave", "valu_issue_frac", "issue_stall_frac",
-                                              "waves_per_simd", "clock_GHz_sq", "l2_hit") if k in iss}
+                                              "waves_per_simd", "waves_dispatched_per_simd", "clock_GHz_sq",
+                                              "l2_hit") if k in iss}
             if r["traffic_frac"] > 0.7:
                 r["limiter"] = "hbm bandwidth"
             elif iss["valu_issue_frac"] > 0.7:
                 r["limiter"] = "valu issue"
             else:
-                r["limiter"] = (f"dependency latency: {iss['waves_per_simd']:.1f} waves/SIMD, "
+                r["limiter"] = (f"dependency latency: {iss['waves_per_simd']:.1f} waves resident per SIMD, "
                                 f"{iss['valu_issue_frac']:.2f} of VALU issue slots, HBM traffic "
                                 f"{r['traffic_frac']:.2f} of peak")
     return r

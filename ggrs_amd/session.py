@@ -253,7 +253,7 @@ class SessionBuilder:
         self._fanout = bool(on)
         return self
 
-    def with_desync_detection_mode(self, interval: int) -> "SessionBuilder":  # builder.rs:167-172
+    def with_desync_detection_mode(self, interval: int) -> "SessionBuilder":  # builder.rs:169-172
         """P2P: DesyncDetection::On{interval} for interval > 0, Off for 0 (default)."""
         if interval < 0:
             raise InvalidRequest("desync detection interval must be >= 0")

@@ -101,7 +101,10 @@ def main():
                 "clock_GHz_grbm": (e["GRBM_GUI_ACTIVE"] / 8.0 / e["avg_ns"]) if e.get("GRBM_GUI_ACTIVE") else None,
                 "valu_issue_frac": e["SQ_INSTS_VALU"] * 2.0 / (1024.0 * cyc),
                 "issue_stall_frac": e.get("SQ_WAIT_INST_ANY", 0.0) / max(1.0, e.get("SQ_WAVE_CYCLES", 1.0)),
-                "waves_per_simd": e.get("SQ_WAVES", 0.0) / 1024.0,
+                "waves_dispatched_per_simd": e.get("SQ_WAVES", 0.0) / 1024.0,
+                # SQ_WAVE_CYCLES counts quad-cycles (MI355X_MICROARCH.md, s_memtime vs SQ PMC units):
+                # the average number of waves resident per SIMD over the kernel
+                "waves_per_simd": e.get("SQ_WAVE_CYCLES", 0.0) * 4.0 / (1024.0 * cyc),
                 "l2_hit": (e["TCC_HIT_sum"] / (e["TCC_HIT_sum"] + e["TCC_MISS_sum"]))
                 if e.get("TCC_HIT_sum") is not None and e.get("TCC_MISS_sum") is not None else None,
             }
