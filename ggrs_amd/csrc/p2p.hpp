@@ -461,6 +461,9 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
   auto player_of = [&](int j) __attribute__((always_inline)) { return kSplit ? lane : j; };
 
   int32_t cur = p.qs[QS_CUR * Spad + s];
+  // cur % W, kept alongside cur (every SaveGameState is of the current frame):
+  // a division by the runtime W costs a dozen VALU instructions
+  unsigned cur_slot = static_cast<unsigned>(cur % p.W);
   int32_t last_saved = p.qs[QS_LAST_SAVED * Spad + s];
   int32_t last_conf = p.qs[QS_LAST_CONF * Spad + s];
   DevQueue q[PPL];
@@ -541,7 +544,11 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
   // re-predicted, but the game never loads, saves or advances.  A dry run
   // reproduces that bookkeeping without touching the game state or the cells.
   bool exec = true;
-  // SaveGameState{cell, frame}: game checksum, cell.save (sync_layer.rs:118-125)
+  auto next_frame = [&]() __attribute__((always_inline)) {  // SyncLayer::advance_frame
+    cur += 1;
+    cur_slot = cur_slot + 1 == static_cast<unsigned>(W) ? 0u : cur_slot + 1;
+  };
+  // SaveGameState{cell, frame = cur}: game checksum, cell.save (sync_layer.rs:118-125)
   auto save = [&](int32_t f) __attribute__((always_inline)) {
     last_saved = f;
     ++nsave;
@@ -550,7 +557,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     CsCtx ctx{0ull, s, nonce++};
     CS c{};
     if constexpr (!(RB_P2P_EXP & 2)) c = G::checksum(w, f, lane, ctx);
-    const unsigned slot = static_cast<unsigned>(f % W);
+    const unsigned slot = cur_slot;  // f == cur
     if constexpr (kLdsC) {
 #pragma unroll
       for (int n = 0; n < NW; ++n) lds_cell[(slot * NW + n) * bd + tid] = w[n];
@@ -615,6 +622,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     }
     load_frame = to_load;
     cur = to_load;
+    cur_slot = slot;
 #pragma unroll
     for (int j = 0; j < PPL; ++j) {  // SyncLayer::reset_prediction
       q[j].pred_frame = kNullFrame;
@@ -624,7 +632,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     for (int32_t i = 0; i < count; ++i) {
       if (kSparse ? cur == min_confirmed : i > 0) save(cur);
       advance(cur);
-      cur += 1;
+      next_frame();
     }
   };
   // Speculative select: when the only misprediction is the speculated
@@ -751,10 +759,16 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
   auto remote_start = [&](int j) __attribute__((always_inline)) {
     return q[j].conn_last == kNullFrame ? p.remote_delay : q[j].conn_last + 1;
   };
+  // remote_in[frame][P][S]: a per-lane base and a 32-bit frame stride (P * S * IB < 2^32),
+  // so an address is one 32x32->64 multiply-add
+  const uint32_t rstride = static_cast<uint32_t>(P) * static_cast<uint32_t>(p.S) * IB;
+  const uint8_t* rbase[PPL];
+#pragma unroll
+  for (int j = 0; j < PPL; ++j)
+    rbase[j] = p.remote_in + (static_cast<size_t>(min(player_of(j), P - 1)) * p.S + s) * IB;
   auto load_remote = [&](int j, int32_t f) __attribute__((always_inline)) -> uint32_t {
-    const int h = min(player_of(j), P - 1);
     f = max(0, min(f, p.remote_frames - 1));
-    const uint8_t* src = p.remote_in + (static_cast<size_t>(f) * P + h) * p.S * IB + static_cast<size_t>(s) * IB;
+    const uint8_t* src = rbase[j] + static_cast<uint64_t>(static_cast<uint32_t>(f)) * rstride;
     return IB == 4 ? *reinterpret_cast<const uint32_t*>(src) : *src;
   };
   // desync detection after set_last_confirmed_frame (p2p_session.rs:313-316):
@@ -898,6 +912,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
       }
     } else {
       const int32_t cur0 = cur, ls0 = last_saved, df0 = disc_frame;
+      const unsigned cs0 = cur_slot;
       DevQueue q0[PPL];
 #pragma unroll
       for (int j = 0; j < PPL; ++j) q0[j] = q[j];
@@ -907,6 +922,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
       threshold = status != kP2PStatusPanic && cur >= W && cur - last_conf >= W;
       if (!threshold && status != kP2PStatusPanic) {
         cur = cur0;
+        cur_slot = cs0;
         last_saved = ls0;
         disc_frame = df0;
 #pragma unroll
@@ -938,7 +954,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
         q[j].conn_last = q_add(q[j], ring, h, s, cur + p.delay, lin[j]);  // local_connect_status[h].last_frame
       }
       advance(cur);
-      cur += 1;
+      next_frame();
     }
 #pragma unroll
     for (int j = 0; j < PPL; ++j) {
