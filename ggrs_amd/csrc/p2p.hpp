@@ -356,11 +356,11 @@ __device__ __forceinline__ void q_add_by_frame(DevQueue& q, const R& r, int h, u
   r.put(f, h, s, v);
   q.last_added = f;
   q.len += 1;
-  if (q.pred_frame != kNullFrame) {
-    if (q.first_inc == kNullFrame && v != q.pred_val) q.first_inc = f;
-    if (q.pred_frame == q.last_req && q.first_inc == kNullFrame) q.pred_frame = kNullFrame;
-    else q.pred_frame += 1;
-  }
+  // the prediction bookkeeping as selects (no branch: every call site is in the hot poll)
+  const bool pr = q.pred_frame != kNullFrame;
+  q.first_inc = (pr && q.first_inc == kNullFrame && v != q.pred_val) ? f : q.first_inc;
+  const bool done = q.pred_frame == q.last_req && q.first_inc == kNullFrame;
+  q.pred_frame = pr ? (done ? kNullFrame : q.pred_frame + 1) : q.pred_frame;
 }
 // input_queue.rs:149-163 + 207-239 add_input with the delay already applied to
 // `f`: replicate the entry before head (blank before the first add) up to f.
