@@ -245,6 +245,9 @@ CASES = [  # game, P, W, d, rd, local_mask, sparse, lag range
     # stubs_enum.rs: the game compares (input, InputStatus) tuples, so Predicted vs Confirmed matters
     (G.Game.STUB_ENUM, 2, 8, 1, 1, 0b01, False, (1, 4)),
     (G.Game.STUB_ENUM, 2, 6, 0, 2, 0b10, True, (0, 5)),
+    # W > 8: the snapshot ring stays in HBM (the LDS ring holds at most 8 cells)
+    (G.Game.EX_GAME, 2, 12, 1, 1, 0b01, False, (1, 9)),
+    (G.Game.EX_GAME, 3, 10, 0, 2, 0b001, True, (1, 7)),
 ]
 
 
