@@ -115,6 +115,37 @@ __device__ __forceinline__ float rem_euclid(float x, float rhs) {
 }
 
 // ----------------------------------------------------------------------------
+// Correctly rounded f32 sqrt and division for operands in known ranges: the
+// sequences the compiler emits under -fhip-fp32-correctly-rounded-divide-sqrt,
+// minus the scaling and special-value fix-ups those ranges never need.
+// ----------------------------------------------------------------------------
+// sqrt(x) for x in (1, +inf]: v_sqrt_f32 (within 1 ulp), then the neighbour
+// test (fma residuals of s - 1 ulp and s + 1 ulp).  The compiler's sequence adds
+// a 2^32 scaling below 2^-96 and a class check for +-0/inf; for x = +inf this
+// one also returns +inf (both residuals are NaN).
+__device__ __forceinline__ float sqrt_rn_above_one(float x) {
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const float sd = __uint_as_float(__float_as_uint(s) - 1u), su = __uint_as_float(__float_as_uint(s) + 1u);
+  const float t = __builtin_fmaf(-sd, s, x) <= 0.0f ? sd : s;
+  return __builtin_fmaf(-su, s, x) > 0.0f ? su : t;
+}
+// 1/d refined once, the reciprocal step of the division sequence.
+__device__ __forceinline__ float rcp_refined(float d) {
+  const float r = __builtin_amdgcn_rcpf(d);
+  return __builtin_fmaf(__builtin_fmaf(-d, r, 1.0f), r, r);
+}
+// n / d with r = rcp_refined(d): the quotient and two residual corrections of
+// the compiler's sequence (v_div_scale / v_div_fmas / v_div_fixup reduce to
+// exactly these fmas when nothing is scaled).  Valid, i.e. nothing would be
+// scaled or fixed up, for d in (1, 256) and 2^-96 <= |n| (so |n/d| is normal
+// and far from overflow).
+__device__ __forceinline__ float div_rn_unscaled(float n, float d, float r) {
+  float q = n * r;
+  q = __builtin_fmaf(__builtin_fmaf(-d, q, n), r, q);
+  return __builtin_fmaf(__builtin_fmaf(-d, q, n), r, q);
+}
+
+// ----------------------------------------------------------------------------
 // fletcher16 closed form pieces
 // ----------------------------------------------------------------------------
 struct Fl16 {

@@ -153,9 +153,16 @@ struct ExGame {
     // the clamp, so it moves inside the branch.
     const float m2 = vx * vx + vy * vy;
     if (m2 > kMaxSpeed * kMaxSpeed) {
-      const float mag = __builtin_sqrtf(m2);
-      vx = (vx * kMaxSpeed) / mag;
-      vy = (vy * kMaxSpeed) / mag;
+      const float mag = sqrt_rn_above_one(m2);
+      const float nx = vx * kMaxSpeed, ny = vy * kMaxSpeed;
+      if (mag < 256.0f && __builtin_fabsf(nx) >= 0x1p-96f && __builtin_fabsf(ny) >= 0x1p-96f) {
+        const float r = rcp_refined(mag);  // both divisions share the denominator
+        vx = div_rn_unscaled(nx, mag, r);
+        vy = div_rn_unscaled(ny, mag, r);
+      } else {  // zeros, tiny or huge operands: the full IEEE division
+        vx = nx / mag;
+        vy = ny / mag;
+      }
     }
   }
 
