@@ -114,6 +114,19 @@ __device__ __forceinline__ float rem_euclid(float x, float rhs) {
   return r < 0.0f ? r + ay : r;
 }
 
+// kNear: the caller guarantees -|rhs| < x < 2|rhs|.  There fmod(x, rhs) is x
+// for x < |rhs| and x - |rhs| (exact) above, so rem_euclid is one add or
+// subtract of |rhs|, the same operation rem_euclid performs on that range.
+template <bool kNear = false>
+__device__ __forceinline__ float rem_euclid_near(float x, float rhs) {
+  if constexpr (kNear) {
+    const float ay = __builtin_fabsf(rhs);
+    return x < 0.0f ? x + ay : (x >= ay ? x - ay : x);
+  } else {
+    return rem_euclid<false>(x, rhs);
+  }
+}
+
 // ----------------------------------------------------------------------------
 // Correctly rounded f32 sqrt and division for operands in known ranges: the
 // sequences the compiler emits under -fhip-fp32-correctly-rounded-divide-sqrt,

@@ -218,14 +218,17 @@ struct ExGame {
   // Every f32 operation is the same one on the same operands as in
   // advance_player, so the results are bit-identical:
   //   up ? v + t : v - t          ==  v + (up ? t : -t)    (IEEE a - b = a + (-b))
+  //   -(S * c)                    ==  (-S) * c             (rounding is sign-symmetric)
+  //   up != down ? v + t : v      ==  v + (up != down ? t : -0.0)
+  //     (v + -0 is v for every v, +-0 included; v is never a signalling NaN
+  //     here: it comes out of the friction multiply, which quiets NaNs)
   //   left ? rot - r : rot + r    ==  rot + (left ? -r : r)
   static constexpr bool kHasPrep = true;
   static constexpr bool kUsesStatus = false;  // reads only Disconnected (status bit i)
   template <int N>
   struct Prep {
-    float tx[kPlayersPerLane][N], ty[kPlayersPerLane][N];  // signed thrust of frame k
+    float tx[kPlayersPerLane][N], ty[kPlayersPerLane][N];  // thrust added in frame k (-0 when none)
     float rot[kPlayersPerLane][N + 1];                       // rotation before frame k (rot[N]: after the last)
-    uint32_t thrust[kPlayersPerLane];                        // bit k: UP xor DOWN at frame k
   };
   template <bool kInRange, int N, class InRecT>
   __device__ static void prepare(const uint32_t (&w)[NWL], const InRecT (&in)[N], int lane, Prep<N>& pr,
@@ -234,18 +237,17 @@ struct ExGame {
     for (int j = 0; j < kPlayersPerLane; ++j) {
       const int i = kSplit ? lane : j;
       float rot = __uint_as_float(w[5 * j + 4]);
-      pr.thrust[j] = 0u;
 #pragma unroll
       for (int k = 0; k < N; ++k) {
         const uint32_t input = player_input(static_cast<InRec>(in[k]), i);
         const bool up = input & 1u, down = input & 2u, left = input & 4u, right = input & 8u;
         pr.rot[j][k] = rot;
         const SinCos sc = sincosf_glibc<kInRange>(rot, unexpected);
-        const float tx = kMovementSpeed * sc.c, ty = kMovementSpeed * sc.s;
-        pr.tx[j][k] = up ? tx : -tx;
-        pr.ty[j][k] = up ? ty : -ty;
-        pr.thrust[j] |= (up != down ? 1u : 0u) << k;
-        const float r1 = rem_euclid<kInRange>(rot + (left ? -kRotationSpeed : kRotationSpeed), 2.0f * kPi);
+        const float sp = up ? kMovementSpeed : -kMovementSpeed;
+        const float tx = sp * sc.c, ty = sp * sc.s;
+        pr.tx[j][k] = up != down ? tx : -0.0f;
+        pr.ty[j][k] = up != down ? ty : -0.0f;
+        const float r1 = rem_euclid_near<kInRange>(rot + (left ? -kRotationSpeed : kRotationSpeed), 2.0f * kPi);
         rot = left != right ? r1 : rot;
       }
       pr.rot[j][N] = rot;
@@ -258,12 +260,8 @@ struct ExGame {
     for (int j = 0; j < kPlayersPerLane; ++j) {
       uint32_t* p = &w[5 * j];
       const float old_x = __uint_as_float(p[0]), old_y = __uint_as_float(p[1]);
-      float vx = __uint_as_float(p[2]) * kFriction;
-      float vy = __uint_as_float(p[3]) * kFriction;
-      const bool th = (pr.thrust[j] >> k) & 1u;
-      const float vx1 = vx + pr.tx[j][k], vy1 = vy + pr.ty[j][k];
-      vx = th ? vx1 : vx;
-      vy = th ? vy1 : vy;
+      float vx = __uint_as_float(p[2]) * kFriction + pr.tx[j][k];
+      float vy = __uint_as_float(p[3]) * kFriction + pr.ty[j][k];
       speed_clamp(vx, vy);
       float x = old_x + vx, y = old_y + vy;
       x = fminf(fmaxf(x, 0.0f), kWidth);
@@ -275,14 +273,19 @@ struct ExGame {
       p[4] = __float_as_uint(pr.rot[j][k + 1]);
     }
   }
-  // Rotations stay in [0, 2pi] once there (rem_euclid), so a state whose every
-  // |rot| < 12 keeps sincos below 120 and rem_euclid's argument below 4pi for
-  // any number of AdvanceFrames: no out-of-line library paths needed.
+  // A rotation in (-6, 6.5) steps to rot +- 2.5/60 in (-2pi, 4pi), which
+  // rem_euclid maps into [0, 2pi] with one add or subtract (rem_euclid_near);
+  // from there every later step stays in that interval.  So a state whose
+  // every rotation is in (-6, 6.5) needs no out-of-line library path (sincos
+  // below 120, no fmodf) for any number of AdvanceFrames.  NaN is out of range.
   static constexpr bool kHasRangePath = true;
   __device__ static bool in_range(const uint32_t (&w)[NWL]) {
     bool ok = true;
 #pragma unroll
-    for (int j = 0; j < kPlayersPerLane; ++j) ok &= __builtin_fabsf(__uint_as_float(w[5 * j + 4])) < 12.0f;
+    for (int j = 0; j < kPlayersPerLane; ++j) {
+      const float r = __uint_as_float(w[5 * j + 4]);
+      ok &= r > -6.0f && r < 6.5f;
+    }
     return ok;
   }
 
@@ -296,8 +299,7 @@ struct ExGame {
     constexpr uint32_t c2 = P * static_cast<uint32_t>((n - 4) + (n - 12) + (n - 20 - 8 * P) + (n - 28 - 16 * P));
     auto wp = [](int o) { return static_cast<uint32_t>(n - o) * 0x01010101u - 0x03020100u; };  // (n-o, n-o-1, n-o-2, n-o-3)
     const bool lead = lane == 0;
-    Fl16 a{lead ? c1 : 0u, lead ? c2 : 0u};
-    fl16_word(a, lead ? static_cast<uint32_t>(frame) : 0u, fl16_weights(n, 0));
+    Fl16 a{lead ? c1 : 0u, lead ? c2 : 0u};  // loop-invariant: hoisted by the compiler
 #pragma unroll
     for (int j = 0; j < kPlayersPerLane; ++j) {
       const int i = kSplit ? lane : j;
@@ -310,6 +312,7 @@ struct ExGame {
     }
     a.s1 = group_sum<kLanes>(a.s1);
     a.s2 = group_sum<kLanes>(a.s2);
+    fl16_word(a, static_cast<uint32_t>(frame), fl16_weights(n, 0));  // the frame word, once per session
     return fl16_finish(a);
   }
 };
