@@ -651,7 +651,9 @@ struct GameOpsT final : GameOps {
     size_t lds = p2p_lds_bytes<G>(block);
     if constexpr (!kSpec && !kNet && p2p_lds_queue<G>()) {
       if (p2p_lds_cells<G>(p.W)) {  // the snapshot ring in LDS (p2p_lds_cell_bytes)
-        auto k = p2p_kernel<G, kSpec, kSparse, kNet, true>;
+        // lane-asynchronous ticks on the plain path unless the batch asked for lock-step ticks
+        auto k = (!kSparse && !p.sync_ticks) ? p2p_kernel<G, kSpec, kSparse, kNet, true, !kSparse>
+                                             : p2p_kernel<G, kSpec, kSparse, kNet, true, false>;
         lds += p2p_lds_cell_bytes<G>(block, p.W);
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                            static_cast<int>(lds));
@@ -660,7 +662,7 @@ struct GameOpsT final : GameOps {
         return hipGetLastError();
       }
     }
-    hipLaunchKernelGGL((p2p_kernel<G, kSpec, kSparse, kNet, false>), dim3(grid), dim3(block), lds, st, p);
+    hipLaunchKernelGGL((p2p_kernel<G, kSpec, kSparse, kNet, false, false>), dim3(grid), dim3(block), lds, st, p);
     return hipGetLastError();
   }
   hipError_t launch_p2p(const P2PParams& p, int block, hipStream_t st) const override {

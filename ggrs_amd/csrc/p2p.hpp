@@ -143,6 +143,7 @@ struct P2PParams {
   int32_t S, Spad, W, delay, remote_delay, T;
   uint32_t local_mask;
   int32_t sparse;
+  int32_t sync_ticks;  // 1: lock-step ticks on the plain path too (no kAsync; A/B and tests)
   DesyncParams ds;
   PeerParams peer;
 };
@@ -422,8 +423,24 @@ __device__ __forceinline__ uint32_t q_input(DevQueue& q, const R& r, int h, unsi
 #ifndef RB_P2P_EXP
 #define RB_P2P_EXP 0
 #endif
-template <class G, bool kSpec, bool kSparse, bool kNet, bool kLdsC>
+// kAsync (plain path with the LDS snapshot ring only): lane-asynchronous
+// ticks.  Every loop iteration a session executes exactly one AdvanceFrame:
+// a resimulated frame of its current rollback ([SaveGameState], its
+// synchronized_inputs, AdvanceFrame), or, once its rollback is done, the rest
+// of the tick (set_last_confirmed_frame, add_local_input, SaveGameState of
+// the current frame) and the tick's new frame.  A session starting a tick
+// first runs the tick's opening (poll, PredictionThreshold, the rollback
+// decision, LoadGameState) in the same iteration.  A wave then iterates max
+// over its sessions of the frames each executes in the launch, instead of the
+// sum over ticks of its deepest rollback (every per-frame step of the
+// rollback, the InputQueue reads included, rides in the same iteration): one
+// session's rollback no longer holds up the other 31.  Each session's own
+// operations run in the reference's order, except that the tick's final
+// SaveGameState moves behind set_last_confirmed_frame and add_local_input,
+// which touch neither the state nor the cells.
+template <class G, bool kSpec, bool kSparse, bool kNet, bool kLdsC, bool kAsync>
 __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
+  static_assert(!kAsync || (kLdsC && !kSparse && !kSpec && !kNet), "lane-asynchronous ticks: plain path, LDS cells");
   using InRec = typename G::InRec;
   using CS = typename G::CS;
   constexpr int NW = G::NWL;
@@ -549,15 +566,10 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     cur_slot = cur_slot + 1 == static_cast<unsigned>(W) ? 0u : cur_slot + 1;
   };
   // SaveGameState{cell, frame = cur}: game checksum, cell.save (sync_layer.rs:118-125)
-  auto save = [&](int32_t f) __attribute__((always_inline)) {
-    last_saved = f;
-    ++nsave;
-    if (!exec) return;
-    ++tot_save;
+  auto store_cell = [&](int32_t f, unsigned slot) __attribute__((always_inline)) {
     CsCtx ctx{0ull, s, nonce++};
     CS c{};
     if constexpr (!(RB_P2P_EXP & 2)) c = G::checksum(w, f, lane, ctx);
-    const unsigned slot = cur_slot;  // f == cur
     if constexpr (kLdsC) {
 #pragma unroll
       for (int n = 0; n < NW; ++n) lds_cell[(slot * NW + n) * bd + tid] = w[n];
@@ -572,6 +584,13 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
         p.tag[slot * Spad + s] = f;
       }
     }
+  };
+  auto save = [&](int32_t f) __attribute__((always_inline)) {
+    last_saved = f;
+    ++nsave;
+    if (!exec) return;
+    ++tot_save;
+    store_cell(f, cur_slot);  // f == cur
   };
   // SyncLayer::synchronized_inputs (sync_layer.rs:187-200) for this lane's
   // players: a disconnected player past its last frame is (zeroed, Disconnected)
@@ -593,23 +612,25 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
   };
   auto advance = [&](int32_t f) __attribute__((always_inline)) {  // AdvanceFrame{inputs}
     uint32_t dmask = 0u;
-    const InRec rec = sync_inputs(f, dmask);
+    const InRec in = sync_inputs(f, dmask);
     ++nadv;
     if (exec) {
-      if constexpr (RB_P2P_EXP & 1) w[0] += static_cast<uint32_t>(rec);  // attribution builds only
-      else G::advance(w, rec, lane, dmask, &p.counters[1]);
+      if constexpr (RB_P2P_EXP & 1) w[0] += static_cast<uint32_t>(in);  // attribution builds only
+      else G::advance(w, in, lane, dmask, &p.counters[1]);
       ++tot_adv;
     }
   };
   // P2PSession::adjust_gamestate (p2p_session.rs:621-673)
-  auto adjust = [&](int32_t first_incorrect, int32_t min_confirmed) __attribute__((always_inline)) {
+  // its opening: the load_frame asserts, LoadGameState, reset_prediction; the
+  // number of frames to resimulate (-1 after a panic)
+  auto adjust_begin = [&](int32_t first_incorrect) __attribute__((always_inline)) -> int32_t {
     const int32_t to_load = kSparse ? last_saved : first_incorrect;
     const int32_t count = cur - to_load;
     const unsigned slot = static_cast<unsigned>(to_load % W);
     const int32_t tag = kLdsC ? lds_tag[slot * bps + sl] : p.tag[slot * Spad + s];
     if (to_load < 0 || to_load > first_incorrect || count <= 0 || count > W || tag != to_load) {
       status = kP2PStatusPanic;  // a reference assert (sync_layer.rs:141-148) would fire
-      return;
+      return -1;
     }
     if (exec) {  // LoadGameState
       if constexpr (kLdsC) {
@@ -629,6 +650,10 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
       q[j].first_inc = kNullFrame;
       q[j].last_req = kNullFrame;
     }
+    return count;
+  };
+  auto adjust = [&](int32_t first_incorrect, int32_t min_confirmed) __attribute__((always_inline)) {
+    const int32_t count = adjust_begin(first_incorrect);
     for (int32_t i = 0; i < count; ++i) {
       if (kSparse ? cur == min_confirmed : i > 0) save(cur);
       advance(cur);
@@ -692,19 +717,33 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
   };
   // advance_frame (p2p_session.rs:253-303) up to the local inputs: frame-0
   // save, rollback, save / sparse check, set_last_confirmed_frame.
-  auto rollback_and_save = [&]() __attribute__((always_inline)) {
+  // the frame-0 save, confirmed_frame (:487-498) and check_simulation_consistency
+  auto rollback_open = [&](int32_t& confirmed, int32_t& first_inc) __attribute__((always_inline)) {
     load_frame = kNullFrame;
     nadv = nsave = 0;
     if (cur == 0) save(cur);
-    int32_t confirmed = INT32_MAX, first_inc = INT32_MAX;
+    confirmed = INT32_MAX;
+    first_inc = INT32_MAX;
 #pragma unroll
     for (int j = 0; j < PPL; ++j) {
-      confirmed = min(confirmed, conn_of(j));  // confirmed_frame (:487-498)
-      if (q[j].first_inc != kNullFrame) first_inc = min(first_inc, q[j].first_inc);  // check_simulation_consistency
+      confirmed = min(confirmed, conn_of(j));
+      if (q[j].first_inc != kNullFrame) first_inc = min(first_inc, q[j].first_inc);
     }
     confirmed = group_min<L>(confirmed);
     first_inc = group_min<L>(first_inc);
     if (disc_frame != kNullFrame) first_inc = min(first_inc, disc_frame);  // session-uniform
+  };
+  // set_last_confirmed_frame (sync_layer.rs:220-244)
+  auto set_last_confirmed = [&](int32_t confirmed) __attribute__((always_inline)) {
+    last_conf = kSparse ? min(confirmed, last_saved) : confirmed;
+    if (last_conf > 0) {
+#pragma unroll
+      for (int j = 0; j < PPL; ++j) q_discard(q[j], last_conf - 1);
+    }
+  };
+  auto rollback_and_save = [&]() __attribute__((always_inline)) {
+    int32_t confirmed, first_inc;
+    rollback_open(confirmed, first_inc);
     if (first_inc != INT32_MAX) {
       if (!(kSpec && exec && try_select(first_inc, confirmed))) adjust(first_inc, confirmed);
       disc_frame = kNullFrame;
@@ -718,11 +757,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     } else {
       save(cur);
     }
-    last_conf = kSparse ? min(confirmed, last_saved) : confirmed;  // set_last_confirmed_frame (sync_layer.rs:220-244)
-    if (last_conf > 0) {
-#pragma unroll
-      for (int j = 0; j < PPL; ++j) q_discard(q[j], last_conf - 1);
-    }
+    set_last_confirmed(confirmed);
     // an InputQueue panic in this tick's resimulation or discard (DevQueue::bad); the advance
     // of the new frame cannot raise one (its frame is above every tail).  Only peers' reports
     // reach those states: without them a queue's tail never passes a frame a rollback reads
@@ -795,10 +830,15 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     for (int k = 0; k < kPre; ++k) rv[j][k] = load_remote(j, f + k);
   }
 
-  for (int t = 0; t < p.T; ++t) {
+  // One tick of the batch for this session (advance_frame and the requests it
+  // returns); false when the session stops on a reference panic.
+  int32_t up_n[PPL];
+  uint32_t lin_n[PPL], rv_n[PPL][kPre];
+  // The tick's opening, through the PredictionThreshold decision: 0 = the
+  // session stopped on a panic, 1 = the tick is over (Err(PredictionThreshold)),
+  // 2 = rollback_and_save, add_local_input and the new frame follow.
+  auto tick_begin = [&](int t) __attribute__((always_inline)) -> int {
     const int tn = t + 1 < p.T ? t + 1 : t;
-    int32_t up_n[PPL];
-    uint32_t lin_n[PPL], rv_n[PPL][kPre];
 #pragma unroll
     for (int j = 0; j < PPL; ++j) {
       up_n[j] = load_upto(tn, j);
@@ -905,7 +945,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
       for (int j = 0; j < PPL; ++j) confirmed = min(confirmed, conn_of(j));
       confirmed = group_min<L>(confirmed);
       threshold = cur >= W && cur - confirmed >= W;
-      if (threshold) {
+      if (threshold) {  // the dropped request list: bookkeeping only
         exec = false;
         rollback_and_save();
         exec = true;
@@ -929,7 +969,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
         for (int j = 0; j < PPL; ++j) q[j] = q0[j];
       }
     }
-    if (status == kP2PStatusPanic) break;
+    if (status == kP2PStatusPanic) return 0;
     if (threshold) {
       status = kP2PStatusThreshold;  // Err(PredictionThreshold): the game does not move this tick
       load_frame = kNullFrame;       // and the user never sees the dropped requests
@@ -937,31 +977,102 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
       if (lead) atomicAdd(&p.counters[0], 1u);
       if (!run_desync()) {  // desync detection ran before add_local_input failed (:313-316, :334)
         status = kP2PStatusPanic;
-        break;
+        return 0;
       }
-    } else {
-      rollback_and_save();
-      if (status == kP2PStatusPanic) break;
-      if (!run_desync()) {
-        status = kP2PStatusPanic;
-        break;
-      }
-      // ---- local inputs: SyncLayer::add_local_input (sync_layer.rs:159-174)
-#pragma unroll
-      for (int j = 0; j < PPL; ++j) {
-        const int h = player_of(j);
-        if (h >= P || !((p.local_mask >> h) & 1u)) continue;
-        q[j].conn_last = q_add(q[j], ring, h, s, cur + p.delay, lin[j]);  // local_connect_status[h].last_frame
-      }
-      advance(cur);
-      next_frame();
+      return 1;
     }
+    return 2;
+  };
+  // ---- local inputs: SyncLayer::add_local_input (sync_layer.rs:159-174)
+  auto add_local = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < PPL; ++j) {
+      const int h = player_of(j);
+      if (h >= P || !((p.local_mask >> h) & 1u)) continue;
+      q[j].conn_last = q_add(q[j], ring, h, s, cur + p.delay, lin[j]);  // local_connect_status[h].last_frame
+    }
+  };
+  auto tick_rotate = [&]() __attribute__((always_inline)) {  // the prefetched deliveries become the next tick's
 #pragma unroll
     for (int j = 0; j < PPL; ++j) {
       up[j] = up_n[j];
       lin[j] = lin_n[j];
 #pragma unroll
       for (int k = 0; k < kPre; ++k) rv[j][k] = rv_n[j][k];
+    }
+  };
+  auto tick = [&](int t) __attribute__((always_inline)) -> bool {
+    const int r = tick_begin(t);
+    if (r == 0) return false;
+    if (r == 2) {
+      rollback_and_save();
+      if (status == kP2PStatusPanic) return false;
+      if (!run_desync()) {
+        status = kP2PStatusPanic;
+        return false;
+      }
+      add_local();
+      advance(cur);
+      next_frame();
+    }
+    tick_rotate();
+    return true;
+  };
+  if constexpr (!kAsync) {
+    for (int t = 0; t < p.T; ++t)
+      if (!tick(t)) break;
+  } else {
+    // lane-asynchronous ticks (see kAsync above): one AdvanceFrame per session per iteration
+    int t = 0, count = 0, i = 0;
+    int32_t confirmed = 0;
+    bool inres = false, stopped = false;
+    [[maybe_unused]] uint32_t iters = 0;
+    while (inres || (!stopped && t < p.T)) {
+      if constexpr (RB_P2P_EXP & 4) ++iters;
+      if (!inres) {  // the next tick's opening, up to its rollback's LoadGameState
+        const int r = tick_begin(t);
+        if (r == 0) {
+          stopped = true;
+        } else if (r == 1) {
+          tick_rotate();
+          ++t;
+        } else {
+          int32_t first_inc;
+          rollback_open(confirmed, first_inc);
+          count = 0;
+          if (first_inc != INT32_MAX) {
+            count = adjust_begin(first_inc);
+            disc_frame = kNullFrame;
+          }
+          if (status == kP2PStatusPanic) stopped = true;
+          else inres = true, i = 0;
+        }
+      }
+      if (inres) {
+        bool save_now, finish = false;
+        if (i < count) {  // resimulated frame i of adjust_gamestate
+          save_now = i > 0;
+          ++i;
+        } else {  // the rest of advance_frame, add_local_input, then the tick's new frame
+          set_last_confirmed(confirmed);
+          add_local();
+          save_now = true;  // rollback_and_save's SaveGameState of the current frame
+          finish = true;
+          inres = false;
+        }
+        if (save_now) save(cur);
+        advance(cur);
+        next_frame();
+        if (finish) {
+          tick_rotate();
+          ++t;
+        }
+      }
+    }
+    if constexpr (RB_P2P_EXP & 4) {  // attribution builds: loop iterations of the wave (max over its lanes)
+#pragma unroll
+      for (int m = 32; m >= 1; m >>= 1) iters = max(iters, static_cast<uint32_t>(__shfl_xor(static_cast<int>(iters), m, 64)));
+      if (__lane_id() == 0) atomicAdd(&p.counters[1], iters);  // reported as the unexpected-path count
     }
   }
 

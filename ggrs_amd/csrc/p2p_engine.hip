@@ -1,6 +1,7 @@
 // ggrs_amd/csrc/p2p_engine.hip — host side of the P2PSession batches
 // (include/ggrs_amd.h rb_p2p_*): buffers, validation (builder.rs), launches of
 // p2p_kernel (p2p.hpp) and the read-backs the parity tests use.
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -26,6 +27,7 @@ struct rb_p2p {
   uint32_t* counters = nullptr;
   unsigned long long* stats = nullptr;  // [ST_COUNT][Spad]
   bool fanout = false;
+  bool sync_ticks = false;  // RB_P2P_SYNC_TICKS=1 at create: lock-step ticks (p2p.hpp kAsync off)
   uint32_t* spec_state = nullptr;
   uint32_t* spec_cells = nullptr;
   void* spec_cs = nullptr;
@@ -228,6 +230,7 @@ rb_status rb_p2p_create(const rb_p2p_config* cfg, rb_p2p** out) {
   if (b->block % 64 != 0 || b->block > 256) return pfail(nullptr, RB_INVALID_REQUEST, "block_size must be 64, 128, 192 or 256");
   b->device = cfg->device;
   b->fanout = fanout;
+  if (const char* e = std::getenv("RB_P2P_SYNC_TICKS")) b->sync_ticks = std::atoi(e) != 0;
   rb_p2p* bp = b.get();
   auto hip_fail = [&](hipError_t e, const char* what) {
     g_p2p_err = std::string(what) + ": " + hipGetErrorString(e);
@@ -381,6 +384,7 @@ rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs,
   p.T = n_ticks;
   p.local_mask = b->cfg.local_mask;
   p.sparse = b->cfg.sparse_saving != 0;
+  p.sync_ticks = b->sync_ticks ? 1 : 0;
   p.spec_on = b->fanout ? 1 : 0;
   p.spec_state = b->spec_state;
   p.spec_cells = b->spec_cells;

@@ -305,6 +305,45 @@ def test_gpu_p2p_fused_launch_equals_per_tick(gpu_available):
         np.testing.assert_array_equal(x, y)
 
 
+FUSED_CASES = [  # game, P, W, d, rd, local_mask, lag range, ticks per launch
+    (G.Game.EX_GAME, 2, 8, 2, 2, 0b01, (0, 6), 16),
+    (G.Game.EX_GAME, 4, 8, 1, 1, 0b0001, (1, 5), 24),
+    (G.Game.EX_GAME, 3, 7, 0, 2, 0b010, (0, 4), 32),
+    (G.Game.EX_GAME, 2, 4, 0, 0, 0b01, (1, 6), 12),  # PredictionThreshold ticks inside the launches
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sync_ticks", [False, True], ids=["async", "lockstep"])
+@pytest.mark.parametrize("case", FUSED_CASES, ids=[f"P{c[1]}-W{c[2]}-d{c[3]}-rd{c[4]}-m{c[5]}-tpl{c[7]}"
+                                                   for c in FUSED_CASES])
+def test_gpu_p2p_fused_launches_match_oracle(gpu_available, monkeypatch, case, sync_ticks):
+    # Multi-tick launches with sessions of different lags, so that inside a launch
+    # sessions sit at different ticks (p2p.hpp kAsync: one AdvanceFrame per session
+    # per iteration) — and the lock-step kernel (RB_P2P_SYNC_TICKS=1): after every
+    # launch the last tick's request counts and every cell, state and queue equal
+    # the oracle's.
+    import torch
+    monkeypatch.setenv("RB_P2P_SYNC_TICKS", "1" if sync_ticks else "0")
+    game, P, W, d, rd, mask, (lo, hi), tpl = case
+    S, T = 300, 96
+    inputs, upto, rin = synth_network(S, P, T, mask, rd, lo, hi)
+    di, du, dr = (torch.from_numpy(a).cuda() for a in (inputs, upto, rin))
+    sess, orc = gpu_pair(game, S, P, W, d, rd, mask, False)
+    for t0 in range(0, T, tpl):
+        t1 = min(T, t0 + tpl)
+        sess.run_ticks(di[t0:t1], du[t0:t1], dr)
+        ost, olf, ona, ons = drive_oracle(orc, mask, inputs, upto, rin, t1, t0=t0)[-1]
+        st, lf, na, ns = sess.status()
+        np.testing.assert_array_equal(st, ost, err_msg=f"status, tick {t1 - 1}")
+        np.testing.assert_array_equal(lf, olf, err_msg=f"LoadGameState frame, tick {t1 - 1}")
+        np.testing.assert_array_equal(na, ona, err_msg=f"AdvanceFrame count, tick {t1 - 1}")
+        np.testing.assert_array_equal(ns, ons, err_msg=f"SaveGameState count, tick {t1 - 1}")
+        compare_state(sess, orc, t1 - 1)
+    assert sess.counters()[2] == 0
+    assert sess.totals()[2] > 0  # rollbacks (LoadGameStates) executed inside the fused launches
+
+
 FANOUT_CASES = [  # P, W, d, rd, local_mask, lag range (BASELINE config 4 = P 4, W 8)
     (4, 8, 1, 1, 0b0001, (1, 5)),
     (2, 8, 2, 2, 0b01, (0, 6)),
