@@ -21,6 +21,7 @@
 
 #include <cmath>
 #include <cstring>
+#include <type_traits>
 
 #include "device_math.hpp"
 
@@ -291,13 +292,18 @@ struct ExGame {
 
   // fletcher16(bincode::serialize(&state)) (ex_game.rs:90-91) from registers:
   // closed-form weighted byte sums per lane, summed over the lane group.
+  // Constant bytes of the image: num_players and the three Vec lengths (u64 =
+  // P, LE) at offsets 4, 12, 20+8P, 28+16P.
+  static constexpr uint32_t kCsC1 = 4u * P;
+  static constexpr uint32_t kCsC2 =
+      P * static_cast<uint32_t>((kImageBytes - 4) + (kImageBytes - 12) + (kImageBytes - 20 - 8 * P) + (kImageBytes - 28 - 16 * P));
+  // (n-o, n-o-1, n-o-2, n-o-3): the weights of the 4 bytes of a word at image offset o
+  __host__ __device__ static constexpr uint32_t wp(int o) {
+    return static_cast<uint32_t>(kImageBytes - o) * 0x01010101u - 0x03020100u;
+  }
   __device__ static CS checksum(const uint32_t (&w)[NWL], int32_t frame, int lane, const CsCtx&) {
     constexpr int n = kImageBytes;
-    // constant bytes: num_players and the three Vec lengths (u64 = P, LE) at
-    // offsets 4, 12, 20+8P, 28+16P
-    constexpr uint32_t c1 = 4u * P;
-    constexpr uint32_t c2 = P * static_cast<uint32_t>((n - 4) + (n - 12) + (n - 20 - 8 * P) + (n - 28 - 16 * P));
-    auto wp = [](int o) { return static_cast<uint32_t>(n - o) * 0x01010101u - 0x03020100u; };  // (n-o, n-o-1, n-o-2, n-o-3)
+    constexpr uint32_t c1 = kCsC1, c2 = kCsC2;
     const bool lead = lane == 0;
     Fl16 a{lead ? c1 : 0u, lead ? c2 : 0u};  // loop-invariant: hoisted by the compiler
 #pragma unroll
@@ -315,6 +321,39 @@ struct ExGame {
     fl16_word(a, static_cast<uint32_t>(frame), fl16_weights(n, 0));  // the frame word, once per session
     return fl16_finish(a);
   }
+
+  // ---- independent players (the speculative fan-out, p2p.hpp
+  // fanout_indep_kernel): State::advance (:259-321) moves every player from its
+  // own input alone, so the players the fan-out does not speculate on follow
+  // one trajectory in all 16 branches and are simulated once per session.
+  // The checksum of a branch cell is then assembled from per-player parts:
+  // fan_partial of each player's words, summed, and fan_finish.
+  static constexpr bool kIndependentPlayers = kSplit;
+  __device__ static Fl16 fan_partial(const uint32_t (&w)[NWL], int i) {  // player i's words (one player per lane)
+    Fl16 a{0u, 0u};
+    fl16_word(a, w[0], wp(off_x(i)));
+    fl16_word(a, w[1], wp(off_x(i) + 4));
+    fl16_word(a, w[2], wp(off_vx(i)));
+    fl16_word(a, w[3], wp(off_vx(i) + 4));
+    fl16_word(a, w[4], wp(off_rot(i)));
+    return a;
+  }
+  __device__ static CS fan_finish(Fl16 a, int32_t frame) {  // + the constant bytes and the frame word
+    a.s1 += kCsC1;
+    a.s2 += kCsC2;
+    fl16_word(a, static_cast<uint32_t>(frame), fl16_weights(kImageBytes, 0));
+    return fl16_finish(a);
+  }
+};
+
+// G::kIndependentPlayers, false for a game that does not declare it
+template <class G, class = void>
+struct IndepPlayers {
+  static constexpr bool value = false;
+};
+template <class G>
+struct IndepPlayers<G, std::void_t<decltype(G::kIndependentPlayers)>> {
+  static constexpr bool value = G::kIndependentPlayers;
 };
 
 // Sum of a u32 over the 64 lanes of a wave (butterfly over ds_swizzle/bpermute);

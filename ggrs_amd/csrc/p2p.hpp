@@ -414,6 +414,17 @@ __device__ __forceinline__ uint32_t q_input(DevQueue& q, const R& r, int h, unsi
   return q.pred_val;  // Predicted
 }
 
+// The speculative fan-out runs fanout_indep_kernel for games whose players move
+// independently (RB_FANOUT_GENERIC=1 builds force fanout_kernel: A/B only).
+#ifndef RB_FANOUT_GENERIC
+#define RB_FANOUT_GENERIC 0
+#endif
+template <class G>
+constexpr bool indep_fanout() {
+  return IndepPlayers<G>::value && !RB_FANOUT_GENERIC;
+}
+constexpr int kIndepLanes = 32;  // lanes per session in fanout_indep_kernel
+
 // kSpec / kSparse / kNet: the fan-out select, sparse saving and the
 // network-fed bookkeeping (desync detection, peers' connect-status reports)
 // are compiled in only where the batch uses them (fewer live scalars: no SGPR
@@ -697,8 +708,12 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     adjust(first_incorrect, min_confirmed);
     exec = true;
     if (status == kP2PStatusPanic) return true;
-    const unsigned Gs = Gpad * kSpecBranches;                              // spec plane width
-    const unsigned col = (s * kSpecBranches + static_cast<unsigned>(kk)) * L + lane;  // branch kk, this lane
+    // branch kk, this lane: column (s * 16 + kk) * L + lane of planes Spad * 16 * L wide; with independent
+    // players (fanout_indep_kernel) column s * 32 + kk of the speculated player's lane, s * 32 + 16 + lane
+    // of any other player's (one trajectory for all branches), planes Spad * 32 wide
+    const unsigned Gs = indep_fanout<G>() ? Spad * kIndepLanes : Gpad * kSpecBranches;
+    const unsigned col = !indep_fanout<G>() ? (s * kSpecBranches + static_cast<unsigned>(kk)) * L + lane
+                         : s * kIndepLanes + (lane == rs ? static_cast<unsigned>(kk) : kSpecBranches + lane);
     const CS* __restrict__ scs = reinterpret_cast<const CS*>(p.spec_cs);
     for (int32_t f = base + 1; f < cur; ++f) {  // the cells adjust would have saved
       const unsigned slot = static_cast<unsigned>(f % W);
@@ -1236,6 +1251,93 @@ __global__ void __launch_bounds__(256) fanout_kernel(const FanParams p) {
   }
   store_words<NW>(p.spec_state, static_cast<int>(Gs), static_cast<int>(g), w);
   if (k == 0 && lane == 0) p.stats[ST_BRANCH * Spad + s] += static_cast<unsigned long long>(frames) * kSpecBranches;
+}
+
+// The fan-out for games whose players move independently (G::kIndependentPlayers,
+// ex_game): the 16 branches differ only in the speculated player's lane, so a
+// session takes 32 lanes — lanes 0-15 the speculated player in branches 0-15,
+// lane 16 + h every other player h once — instead of 16 x L.  Cells and states
+// go to column s * 32 + lane of planes Spad * 32 wide (the spec buffers hold
+// Spad * 16 * L >= Spad * 32 columns), so a session's stores are one
+// contiguous run per plane; try_select reads that layout.  Each branch cell's
+// checksum is assembled from the branch lane's part and the sum of the other
+// players' parts.
+template <class G>
+__global__ void __launch_bounds__(256) fanout_indep_kernel(const FanParams p) {
+  using InRec = typename G::InRec;
+  using CS = typename G::CS;
+  constexpr int NW = G::NWL;
+  constexpr int L = G::kLanes;
+  constexpr int P = G::kPlayers, IB = G::kInputBytes;
+  static_assert(IndepPlayers<G>::value && L > 1 && P <= kIndepLanes - kSpecBranches, "independent players, one per lane");
+  const unsigned g = blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned s = g / kIndepLanes;
+  const int r = static_cast<int>(g % kIndepLanes);
+  if (s >= static_cast<unsigned>(p.S)) return;  // the session's 32 lanes leave together
+  const unsigned Spad = static_cast<unsigned>(p.Spad), Gpad = Spad * L;
+  const unsigned Gs = Spad * kIndepLanes;  // spec plane width in this layout
+  const int W = p.W;
+  const RingIO<IB> ring{const_cast<uint8_t*>(reinterpret_cast<const uint8_t*>(p.ring)), P, p.Spad};
+  auto qrow = [&](int field, int h) { return p.qs[static_cast<size_t>(QS_PLAYER0 + field * 4 + h) * Spad + s]; };
+  const int32_t cur = p.qs[QS_CUR * Spad + s];
+  int rs = -1;  // the remote handle with the oldest last added input (ties: lowest handle), as fanout_kernel
+  int32_t la_rs = INT32_MAX;
+#pragma unroll
+  for (int h = 0; h < P; ++h) {
+    if ((p.local_mask >> h) & 1u) continue;
+    const int32_t la = qrow(QF_LAST_ADDED, h);
+    const int32_t key = la == kNullFrame ? -1 : la;
+    if (key < la_rs) {
+      la_rs = key;
+      rs = h;
+    }
+  }
+  bool any_disc = false;
+#pragma unroll
+  for (int h = 0; h < P; ++h) any_disc |= qrow(QF_DISC, h) != 0;
+  const int32_t base = la_rs + 1;
+  const bool valid = p.status[s] != kP2PStatusPanic && !any_disc && rs >= 0 && base < cur && base + W > cur && base >= 0 &&
+                     p.tag[static_cast<unsigned>(base % W) * Spad + s] == base;
+  if (r == 0) {
+    p.spec_meta[SM_BASE * Spad + s] = base;
+    p.spec_meta[SM_END * Spad + s] = cur;
+    p.spec_meta[SM_PLAYER * Spad + s] = rs;
+    p.spec_meta[SM_VALID * Spad + s] = valid ? 1 : 0;
+  }
+  if (!valid) return;  // session-uniform
+  const bool branch = r < kSpecBranches;
+  const int k = branch ? r : 0;
+  const int h = branch ? rs : r - kSpecBranches;  // this lane's player
+  const bool active = branch || (h < P && h != rs);
+  const int hh = h < P ? h : 0;                   // an idle lane reads player 0's data and stores nothing
+  uint32_t w[NW];
+  load_words<NW>(p.snap + static_cast<unsigned>(base % W) * NW * Gpad, static_cast<int>(Gpad), static_cast<int>(s * L + hh), w);
+  const bool local = (p.local_mask >> hh) & 1u;
+  const int32_t la_h = qrow(QF_LAST_ADDED, hh);
+  const uint32_t pred = la_h == kNullFrame ? 0u : ring.get(la_h, hh, s);
+  const unsigned col = g;  // s * 32 + r
+  CS* __restrict__ cs = reinterpret_cast<CS*>(p.spec_cs);
+  uint32_t frames = 0;
+  for (int32_t f = base; f < cur; ++f) {
+    if (f > base) {  // SaveGameState of frame f in every branch
+      Fl16 a = active ? G::fan_partial(w, hh) : Fl16{0u, 0u};
+      // the other players' parts: lanes 16-19 of the session are one DPP quad; their sum to every lane
+      uint32_t o1 = group_sum<4>(branch ? 0u : a.s1), o2 = group_sum<4>(branch ? 0u : a.s2);
+      o1 = static_cast<uint32_t>(__shfl(static_cast<int>(o1), kSpecBranches, kIndepLanes));
+      o2 = static_cast<uint32_t>(__shfl(static_cast<int>(o2), kSpecBranches, kIndepLanes));
+      const unsigned slot = static_cast<unsigned>(f % W);
+      if (active) store_words<NW>(p.spec_cells + slot * NW * Gs, static_cast<int>(Gs), static_cast<int>(col), w);
+      if (branch) cs[(slot * Spad + s) * kSpecBranches + k] = G::fan_finish(Fl16{a.s1 + o1, a.s2 + o2}, f);
+    }
+    uint32_t v;
+    if (branch) v = static_cast<uint32_t>(k);
+    else if (local || (la_h != kNullFrame && f <= la_h)) v = ring.get(f, hh, s);  // Confirmed
+    else v = pred;  // repeat-last prediction (blank before the first input)
+    G::advance(w, static_cast<InRec>(static_cast<uint64_t>(v) << (8 * IB * hh)), hh, 0u, &p.counters[1]);
+    ++frames;
+  }
+  if (active) store_words<NW>(p.spec_state, static_cast<int>(Gs), static_cast<int>(col), w);
+  if (r == 0) p.stats[ST_BRANCH * Spad + s] += static_cast<unsigned long long>(frames) * kSpecBranches;
 }
 
 }  // namespace rb
