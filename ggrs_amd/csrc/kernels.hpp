@@ -680,11 +680,14 @@ struct GameOpsT final : GameOps {
   }
   static constexpr bool kFanout = G::kLanes > 1 && G::kLanes <= 4;
   hipError_t launch_fanout(const FanParams& p, int block, hipStream_t st) const override {
-    if constexpr (kFanout && indep_fanout<G>()) {  // the players the fan-out does not speculate on, once
-      const int grid = (p.Spad * kIndepLanes + block - 1) / block;
-      hipLaunchKernelGGL(fanout_indep_kernel<G>, dim3(grid), dim3(block), 0, st, p);
-      return hipGetLastError();
-    } else if constexpr (kFanout) {
+    if constexpr (kFanout && IndepPlayers<G>::value) {  // the players the fan-out does not speculate on, once
+      if (!p.fan_generic) {
+        const int grid = (p.Spad * kIndepLanes + block - 1) / block;
+        hipLaunchKernelGGL(fanout_indep_kernel<G>, dim3(grid), dim3(block), 0, st, p);
+        return hipGetLastError();
+      }
+    }
+    if constexpr (kFanout) {
       const int grid = (p.Spad * kSpecBranches * G::kLanes + block - 1) / block;
       hipLaunchKernelGGL(fanout_kernel<G>, dim3(grid), dim3(block), 0, st, p);
       return hipGetLastError();

@@ -134,6 +134,7 @@ struct P2PParams {
   const void* spec_cs;         // [W][Spad][16] CS
   const int32_t* spec_meta;    // [SM_COUNT][Spad]
   int32_t spec_on;
+  int32_t fan_generic;  // the branches were left by fanout_kernel, not fanout_indep_kernel
   const uint8_t* local_in;  // tick t, handle h: local_in + t * local_stride + (h * S + s) * IB
   int64_t local_stride;
   const int32_t* upto;      // tick t, handle h: upto[t * upto_stride + h * S + s]
@@ -415,14 +416,8 @@ __device__ __forceinline__ uint32_t q_input(DevQueue& q, const R& r, int h, unsi
 }
 
 // The speculative fan-out runs fanout_indep_kernel for games whose players move
-// independently (RB_FANOUT_GENERIC=1 builds force fanout_kernel: A/B only).
-#ifndef RB_FANOUT_GENERIC
-#define RB_FANOUT_GENERIC 0
-#endif
-template <class G>
-constexpr bool indep_fanout() {
-  return IndepPlayers<G>::value && !RB_FANOUT_GENERIC;
-}
+// independently, unless the batch asks for the generic fanout_kernel
+// (fan_generic: RB_FANOUT_GENERIC=1 at create, for A/B and tests).
 constexpr int kIndepLanes = 32;  // lanes per session in fanout_indep_kernel
 
 // kSpec / kSparse / kNet: the fan-out select, sparse saving and the
@@ -711,9 +706,10 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     // branch kk, this lane: column (s * 16 + kk) * L + lane of planes Spad * 16 * L wide; with independent
     // players (fanout_indep_kernel) column s * 32 + kk of the speculated player's lane, s * 32 + 16 + lane
     // of any other player's (one trajectory for all branches), planes Spad * 32 wide
-    const unsigned Gs = indep_fanout<G>() ? Spad * kIndepLanes : Gpad * kSpecBranches;
-    const unsigned col = !indep_fanout<G>() ? (s * kSpecBranches + static_cast<unsigned>(kk)) * L + lane
-                         : s * kIndepLanes + (lane == rs ? static_cast<unsigned>(kk) : kSpecBranches + lane);
+    const bool indep = IndepPlayers<G>::value && !p.fan_generic;
+    const unsigned Gs = indep ? Spad * kIndepLanes : Gpad * kSpecBranches;
+    const unsigned col = !indep ? (s * kSpecBranches + static_cast<unsigned>(kk)) * L + lane
+                                : s * kIndepLanes + (lane == rs ? static_cast<unsigned>(kk) : kSpecBranches + lane);
     const CS* __restrict__ scs = reinterpret_cast<const CS*>(p.spec_cs);
     for (int32_t f = base + 1; f < cur; ++f) {  // the cells adjust would have saved
       const unsigned slot = static_cast<unsigned>(f % W);
@@ -1172,6 +1168,7 @@ struct FanParams {
   uint32_t* counters;
   int32_t S, Spad, W;
   uint32_t local_mask;
+  int32_t fan_generic;  // fanout_kernel even for independent players
 };
 
 template <class G>

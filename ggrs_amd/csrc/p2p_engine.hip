@@ -27,7 +27,8 @@ struct rb_p2p {
   uint32_t* counters = nullptr;
   unsigned long long* stats = nullptr;  // [ST_COUNT][Spad]
   bool fanout = false;
-  bool sync_ticks = false;  // RB_P2P_SYNC_TICKS=1 at create: lock-step ticks (p2p.hpp kAsync off)
+  bool sync_ticks = false;   // RB_P2P_SYNC_TICKS=1 at create: lock-step ticks (p2p.hpp kAsync off)
+  bool fan_generic = false;  // RB_FANOUT_GENERIC=1 at create: fanout_kernel for every game
   uint32_t* spec_state = nullptr;
   uint32_t* spec_cells = nullptr;
   void* spec_cs = nullptr;
@@ -231,6 +232,7 @@ rb_status rb_p2p_create(const rb_p2p_config* cfg, rb_p2p** out) {
   b->device = cfg->device;
   b->fanout = fanout;
   if (const char* e = std::getenv("RB_P2P_SYNC_TICKS")) b->sync_ticks = std::atoi(e) != 0;
+  if (const char* e = std::getenv("RB_FANOUT_GENERIC")) b->fan_generic = std::atoi(e) != 0;
   rb_p2p* bp = b.get();
   auto hip_fail = [&](hipError_t e, const char* what) {
     g_p2p_err = std::string(what) + ": " + hipGetErrorString(e);
@@ -385,6 +387,7 @@ rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs,
   p.local_mask = b->cfg.local_mask;
   p.sparse = b->cfg.sparse_saving != 0;
   p.sync_ticks = b->sync_ticks ? 1 : 0;
+  p.fan_generic = b->fan_generic ? 1 : 0;
   p.spec_on = b->fanout ? 1 : 0;
   p.spec_state = b->spec_state;
   p.spec_cells = b->spec_cells;
@@ -408,6 +411,7 @@ rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs,
   fp.Spad = b->Spad;
   fp.W = b->W;
   fp.local_mask = b->cfg.local_mask;
+  fp.fan_generic = b->fan_generic ? 1 : 0;
   P2P_TRY(b, hipSetDevice(b->device));
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (b->prof) {

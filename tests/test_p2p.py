@@ -353,13 +353,17 @@ FANOUT_CASES = [  # P, W, d, rd, local_mask, lag range (BASELINE config 4 = P 4,
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("generic", [False, True], ids=["indep", "generic"])
 @pytest.mark.parametrize("case", FANOUT_CASES, ids=[f"P{c[0]}-W{c[1]}-d{c[2]}-rd{c[3]}-m{c[4]}" for c in FANOUT_CASES])
-def test_gpu_speculative_fanout_matches_rollback(gpu_available, case):
+def test_gpu_speculative_fanout_matches_rollback(gpu_available, monkeypatch, case, generic):
     # With the fan-out, matching mispredictions are served by a branch select:
     # statuses, logical request counts, cells and states must stay identical to
     # the reference's rollback (the oracle) on every tick, and selects must
-    # actually happen.
+    # actually happen.  ex_game's players move independently, so the batch runs
+    # fanout_indep_kernel; RB_FANOUT_GENERIC=1 makes it run the generic
+    # fanout_kernel (16 branches x every player) instead.
     import torch
+    monkeypatch.setenv("RB_FANOUT_GENERIC", "1" if generic else "0")
     P, W, d, rd, mask, (lo, hi) = case
     S, T = 96, 80
     inputs, upto, rin = synth_network(S, P, T, mask, rd, lo, hi)

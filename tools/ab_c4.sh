@@ -1,12 +1,12 @@
 #!/bin/bash
-# A/B of the C4 (speculative fan-out) bench line across library builds, interleaved:
-# VARS="fangen cur" (cur = the in-tree build; others ggrs_amd/var/lib_<v>.so).
+# A/B of the C4 (speculative fan-out) bench line, interleaved: the generic
+# fanout_kernel (RB_FANOUT_GENERIC=1) vs fanout_indep_kernel (the default for ex_game).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 for rep in 1 2; do
-  for v in ${VARS:-fangen cur}; do
-    lib=$PWD/ggrs_amd/var/lib_$v.so; [ "$v" = cur ] && lib=$PWD/ggrs_amd/libggrs_amd.so
-    GGRS_AMD_LIB=$lib timeout -k 10 200 python3 -u bench.py --session p2p --num-players 4 --fanout --steps 100 --warmup 16 \
+  for v in generic indep; do
+    gen=0; [ "$v" = generic ] && gen=1
+    RB_FANOUT_GENERIC=$gen timeout -k 10 200 python3 -u bench.py --session p2p --num-players 4 --fanout --steps 100 --warmup 16 \
       --no-cpu-baseline > gpurun_out/abc4_$v.log 2>&1 || exit $?
     python3 -c "
 import json
