@@ -66,14 +66,18 @@ __device__ __noinline__ SinCos sincosf_large(float y, uint32_t* unexpected) {
   return r;
 }
 
-// kInRange: the caller guarantees |y| < 120 (no out-of-line library path).
+// kInRange: the caller guarantees 0 <= y < 6.5 (no out-of-line library path).
 template <bool kInRange = false>
 __device__ __forceinline__ SinCos sincosf_glibc(float y, uint32_t* unexpected) {
   // |y| < pi/4 takes glibc's unreduced branch: reduce_fast yields n = 0 and
   // xr = y exactly there, so one straight-line path serves both.
   const double hpi_inv = 0x1.45F306DC9C883p+23, hpi = 0x1.921FB54442D18p0;  // !TOINT_INTRINSICS form (x86_64)
   const double x = y;
-  const int n = (static_cast<int32_t>(x * hpi_inv) + 0x800000) >> 24;
+  // reduce_fast's quadrant n = ((int)(x * 2^24 * 2/pi) + 2^23) >> 24; for 0 <= y < 6.5 it equals
+  // (int)(y * (float)(2/pi) + 0.5f) with one f32 fma, for every float there
+  // (tests/check_sincos_quadrant.c, run by tests/test_oracle.py)
+  const int n = kInRange ? static_cast<int32_t>(__builtin_fmaf(y, 0x1.45f306p-1f, 0.5f))
+                         : (static_cast<int32_t>(x * hpi_inv) + 0x800000) >> 24;
   double xr = __builtin_fma(-static_cast<double>(n), hpi, x);
   const double x2 = xr * xr;
   // sign[4] = {1,-1,-1,1}: negate when (n & 3) is 1 or 2, i.e. bit 1 of n + 1.

@@ -231,16 +231,19 @@ struct ExGame {
     float tx[kPlayersPerLane][N], ty[kPlayersPerLane][N];  // thrust added in frame k (-0 when none)
     float rot[kPlayersPerLane][N + 1];                       // rotation before frame k (rot[N]: after the last)
   };
-  template <bool kInRange, int N, class InRecT>
-  __device__ static void prepare(const uint32_t (&w)[NWL], const InRecT (&in)[N], int lane, Prep<N>& pr,
-                                 uint32_t* unexpected) {
+  // The inputs as a lane sees them: its player's byte (one player per lane), or
+  // the whole record (every player in one lane).
+  __device__ static uint32_t lane_input(InRec rec, int lane) {
+    return kSplit ? player_input(rec, lane) : static_cast<uint32_t>(rec);
+  }
+  template <bool kInRange, int N>
+  __device__ static void prepare(const uint32_t (&w)[NWL], const uint32_t (&lin)[N], Prep<N>& pr, uint32_t* unexpected) {
 #pragma unroll
     for (int j = 0; j < kPlayersPerLane; ++j) {
-      const int i = kSplit ? lane : j;
       float rot = __uint_as_float(w[5 * j + 4]);
 #pragma unroll
       for (int k = 0; k < N; ++k) {
-        const uint32_t input = player_input(static_cast<InRec>(in[k]), i);
+        const uint32_t input = kSplit ? lin[k] : player_input(static_cast<InRec>(lin[k]), j);
         const bool up = input & 1u, down = input & 2u, left = input & 4u, right = input & 8u;
         pr.rot[j][k] = rot;
         const SinCos sc = sincosf_glibc<kInRange>(rot, unexpected);
@@ -274,18 +277,20 @@ struct ExGame {
       p[4] = __float_as_uint(pr.rot[j][k + 1]);
     }
   }
-  // A rotation in (-6, 6.5) steps to rot +- 2.5/60 in (-2pi, 4pi), which
+  // A rotation in [0, 6.5) steps to rot +- 2.5/60 in (-2pi, 4pi), which
   // rem_euclid maps into [0, 2pi] with one add or subtract (rem_euclid_near);
   // from there every later step stays in that interval.  So a state whose
-  // every rotation is in (-6, 6.5) needs no out-of-line library path (sincos
-  // below 120, no fmodf) for any number of AdvanceFrames.  NaN is out of range.
+  // every rotation is in [0, 6.5) needs no out-of-line library path (sincos
+  // below 120, no fmodf) for any number of AdvanceFrames, and every sincos
+  // argument is in [0, 6.5) (sincosf_glibc's in-range reduction).  NaN is out
+  // of range.
   static constexpr bool kHasRangePath = true;
   __device__ static bool in_range(const uint32_t (&w)[NWL]) {
     bool ok = true;
 #pragma unroll
     for (int j = 0; j < kPlayersPerLane; ++j) {
       const float r = __uint_as_float(w[5 * j + 4]);
-      ok &= r > -6.0f && r < 6.5f;
+      ok &= r >= 0.0f && r < 6.5f;
     }
     return ok;
   }

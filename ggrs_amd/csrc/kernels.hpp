@@ -412,6 +412,13 @@ __global__ void __launch_bounds__(256) steady_kernel(const RunParams p) {
   InRec win[CD + 1];  // inputs of frames f0 .. f0+CD
 #pragma unroll
   for (int k = 0; k <= CD; ++k) win[k] = input_of_frame(f0 + k);
+  // the phase-split games read the window through this lane's view of each input
+  // (ex_game: the lane's player's byte), taken once as an input enters the window
+  [[maybe_unused]] uint32_t lin[CD + 1];
+  if constexpr (G::kHasPrep) {
+#pragma unroll
+    for (int k = 0; k <= CD; ++k) lin[k] = G::lane_input(win[k], lane);
+  }
   CS fsw[NF];  // SyncTest first-seen checksums of frames f0+1 .. f0+CD-1
 #pragma unroll
   for (int k = 1; k < CD; ++k) fsw[k - 1] = fsa[slot_of(f0 + k) * Spad + s];
@@ -461,7 +468,7 @@ __global__ void __launch_bounds__(256) steady_kernel(const RunParams p) {
     constexpr bool kInRange = decltype(in_range_tag)::value;
     [[maybe_unused]] PrepOf<G, CD + 1> prep;
     if constexpr (G::kHasPrep && !kExp)  // the tick's rotation chain and thrust first (games.hpp)
-      G::template prepare<kInRange, CD + 1>(w, win, lane, prep, &p.counters[1]);
+      G::template prepare<kInRange, CD + 1>(w, lin, prep, &p.counters[1]);
 #pragma unroll
     for (int k = 0; k <= CD; ++k) {
       const int f = f0 + k;
@@ -534,6 +541,11 @@ __global__ void __launch_bounds__(256) steady_kernel(const RunParams p) {
 #pragma unroll
     for (int k = 0; k < CD; ++k) win[k] = win[k + 1];
     win[CD] = next_last;
+    if constexpr (G::kHasPrep) {
+#pragma unroll
+      for (int k = 0; k < CD; ++k) lin[k] = lin[k + 1];
+      lin[CD] = G::lane_input(next_last, lane);
+    }
     newin = newin_next;
 #pragma unroll
     for (int k = 0; k + 1 < NF; ++k) fsw[k] = fsw[k + 1];

@@ -135,3 +135,15 @@ def test_speed_clamp_compare_without_sqrt():
                          np.array([0.0, 49.0, np.inf, np.nan], np.float32)])
     with np.errstate(invalid="ignore"):
         assert ((np.sqrt(m2) > np.float32(7.0)) == (m2 > np.float32(49.0))).all()
+
+
+def test_sincos_quadrant_f32_equals_glibc_reduction(tmp_path):
+    # device_math.hpp sincosf_glibc<kInRange> takes glibc's reduce_fast quadrant
+    # from one f32 fma on [0, 6.5) (the range games.hpp ExGame::in_range admits):
+    # checked here for every float of that range (about 4 s).
+    src = os.path.join(os.path.dirname(os.path.abspath(__file__)), "check_sincos_quadrant.c")
+    exe = str(tmp_path / "check_sincos_quadrant")
+    subprocess.run(["gcc", "-O2", "-o", exe, src, "-lm"], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout
+    assert r.stdout.startswith("1087373312 floats, 0 mismatches")
