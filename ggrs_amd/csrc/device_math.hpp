@@ -66,7 +66,9 @@ __device__ __noinline__ SinCos sincosf_large(float y, uint32_t* unexpected) {
   return r;
 }
 
-// kInRange: the caller guarantees 0 <= y < 6.5 (no out-of-line library path).
+// kInRange: the caller guarantees +0 <= y < 6.5 (no out-of-line library path,
+// and no tiny-argument branch: on that range this evaluation without it equals
+// glibc's sinf/cosf for every float, tests/check_sincos_inrange.c).
 template <bool kInRange = false>
 __device__ __forceinline__ SinCos sincosf_glibc(float y, uint32_t* unexpected) {
   // |y| < pi/4 takes glibc's unreduced branch: reduce_fast yields n = 0 and
@@ -95,13 +97,14 @@ __device__ __forceinline__ SinCos sincosf_glibc(float y, uint32_t* unexpected) {
   r.c = (n & 1) ? sp : cp;
   // |y| < 2^-12: glibc returns (y, 1).  Inline: ex_game's rotations sit at
   // exactly 0 for long stretches (State::new gives player 1 rot = 0).
-  const uint32_t top = abstop12(y);
-  if (top < abstop12(0x1p-12f)) {
-    r.s = y;
-    r.c = 1.0f;
-  }
-  if constexpr (!kInRange)
+  if constexpr (!kInRange) {
+    const uint32_t top = abstop12(y);
+    if (top < abstop12(0x1p-12f)) {
+      r.s = y;
+      r.c = 1.0f;
+    }
     if (__builtin_expect(top >= abstop12(120.0f), 0)) r = sincosf_large(y, unexpected);
+  }
   return r;
 }
 

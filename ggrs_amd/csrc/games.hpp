@@ -277,20 +277,20 @@ struct ExGame {
       p[4] = __float_as_uint(pr.rot[j][k + 1]);
     }
   }
-  // A rotation in [0, 6.5) steps to rot +- 2.5/60 in (-2pi, 4pi), which
-  // rem_euclid maps into [0, 2pi] with one add or subtract (rem_euclid_near);
-  // from there every later step stays in that interval.  So a state whose
-  // every rotation is in [0, 6.5) needs no out-of-line library path (sincos
-  // below 120, no fmodf) for any number of AdvanceFrames, and every sincos
-  // argument is in [0, 6.5) (sincosf_glibc's in-range reduction).  NaN is out
-  // of range.
+  // A rotation in [+0, 6.5) steps to rot +- 2.5/60 in (-2pi, 4pi), which
+  // rem_euclid maps into [+0, 2pi] with one add or subtract (rem_euclid_near;
+  // never -0); from there every later step stays in that interval.  So a state
+  // whose every rotation is in [+0, 6.5) needs no out-of-line library path
+  // (sincos below 120, no fmodf) for any number of AdvanceFrames, and every
+  // sincos argument is in [+0, 6.5) (sincosf_glibc's in-range evaluation).
+  // Tested on the bits: -0, negatives and NaN are out of range.
   static constexpr bool kHasRangePath = true;
   __device__ static bool in_range(const uint32_t (&w)[NWL]) {
     bool ok = true;
 #pragma unroll
     for (int j = 0; j < kPlayersPerLane; ++j) {
       const float r = __uint_as_float(w[5 * j + 4]);
-      ok &= r >= 0.0f && r < 6.5f;
+      ok &= __float_as_uint(r) < 0x40D00000u;  // +0 <= r < 6.5f
     }
     return ok;
   }

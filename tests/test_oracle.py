@@ -147,3 +147,15 @@ def test_sincos_quadrant_f32_equals_glibc_reduction(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout
     assert r.stdout.startswith("1087373312 floats, 0 mismatches")
+
+
+def test_sincos_in_range_evaluation_equals_glibc(tmp_path):
+    # device_math.hpp sincosf_glibc<kInRange> (f32 quadrant, no tiny-argument
+    # branch) against this host's glibc sinf/cosf for every float in [+0, 6.5)
+    # (OpenMP, a few seconds on 8 cores).
+    src = os.path.join(os.path.dirname(os.path.abspath(__file__)), "check_sincos_inrange.c")
+    exe = str(tmp_path / "check_sincos_inrange")
+    subprocess.run(["gcc", "-O2", "-fopenmp", "-o", exe, src, "-lm"], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout
+    assert r.stdout.startswith("1087373312 floats, 0 mismatches")
