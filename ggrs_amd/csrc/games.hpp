@@ -231,28 +231,43 @@ struct ExGame {
     float tx[kPlayersPerLane][N], ty[kPlayersPerLane][N];  // thrust added in frame k (-0 when none)
     float rot[kPlayersPerLane][N + 1];                       // rotation before frame k (rot[N]: after the last)
   };
-  // The inputs as a lane sees them: its player's byte (one player per lane), or
-  // the whole record (every player in one lane).
-  __device__ static uint32_t lane_input(InRec rec, int lane) {
-    return kSplit ? player_input(rec, lane) : static_cast<uint32_t>(rec);
+  // One frame's input as this lane's players act on it (decoded once, when the
+  // input enters the steady kernel's window): the signed thrust speed, the
+  // signed rotation step, and all-ones masks for "UP xor DOWN" and "LEFT xor
+  // RIGHT" (bit selects, no compare per use).
+  struct Dec {
+    float sp[kPlayersPerLane], rd[kPlayersPerLane];
+    uint32_t thm[kPlayersPerLane], rom[kPlayersPerLane];
+  };
+  __device__ static Dec decode(InRec rec, int lane) {
+    Dec d;
+#pragma unroll
+    for (int j = 0; j < kPlayersPerLane; ++j) {
+      const uint32_t input = player_input(rec, kSplit ? lane : j);
+      const bool up = input & 1u, down = input & 2u, left = input & 4u, right = input & 8u;
+      d.sp[j] = up ? kMovementSpeed : -kMovementSpeed;
+      d.rd[j] = left ? -kRotationSpeed : kRotationSpeed;
+      d.thm[j] = up != down ? ~0u : 0u;
+      d.rom[j] = left != right ? ~0u : 0u;
+    }
+    return d;
   }
   template <bool kInRange, int N>
-  __device__ static void prepare(const uint32_t (&w)[NWL], const uint32_t (&lin)[N], Prep<N>& pr, uint32_t* unexpected) {
+  __device__ static void prepare(const uint32_t (&w)[NWL], const Dec (&dec)[N], Prep<N>& pr, uint32_t* unexpected) {
 #pragma unroll
     for (int j = 0; j < kPlayersPerLane; ++j) {
       float rot = __uint_as_float(w[5 * j + 4]);
 #pragma unroll
       for (int k = 0; k < N; ++k) {
-        const uint32_t input = kSplit ? lin[k] : player_input(static_cast<InRec>(lin[k]), j);
-        const bool up = input & 1u, down = input & 2u, left = input & 4u, right = input & 8u;
+        const Dec& d = dec[k];
         pr.rot[j][k] = rot;
         const SinCos sc = sincosf_glibc<kInRange>(rot, unexpected);
-        const float sp = up ? kMovementSpeed : -kMovementSpeed;
-        const float tx = sp * sc.c, ty = sp * sc.s;
-        pr.tx[j][k] = up != down ? tx : -0.0f;
-        pr.ty[j][k] = up != down ? ty : -0.0f;
-        const float r1 = rem_euclid_near<kInRange>(rot + (left ? -kRotationSpeed : kRotationSpeed), 2.0f * kPi);
-        rot = left != right ? r1 : rot;
+        const float tx = d.sp[j] * sc.c, ty = d.sp[j] * sc.s;
+        // thrust ? t : -0.0 as a bit select on the mask
+        pr.tx[j][k] = __uint_as_float((d.thm[j] & __float_as_uint(tx)) | (~d.thm[j] & 0x80000000u));
+        pr.ty[j][k] = __uint_as_float((d.thm[j] & __float_as_uint(ty)) | (~d.thm[j] & 0x80000000u));
+        const float r1 = rem_euclid_near<kInRange>(rot + d.rd[j], 2.0f * kPi);
+        rot = __uint_as_float((d.rom[j] & __float_as_uint(r1)) | (~d.rom[j] & __float_as_uint(rot)));
       }
       pr.rot[j][N] = rot;
     }

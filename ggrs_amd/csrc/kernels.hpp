@@ -341,6 +341,16 @@ struct PrepSel<G, N, true> {
 };
 template <class G, int N>
 using PrepOf = typename PrepSel<G, N>::type;
+template <class G, bool = G::kHasPrep>
+struct DecSel {
+  struct type {};
+};
+template <class G>
+struct DecSel<G, true> {
+  using type = typename G::Dec;
+};
+template <class G>
+using DecOf = typename DecSel<G>::type;
 
 // kExp: attribution experiments (RunParams::debug knobs, tools/exp_steady.py);
 // instantiated only in builds made with RB_EXPERIMENTS=1, never in the product.
@@ -412,12 +422,12 @@ __global__ void __launch_bounds__(256) steady_kernel(const RunParams p) {
   InRec win[CD + 1];  // inputs of frames f0 .. f0+CD
 #pragma unroll
   for (int k = 0; k <= CD; ++k) win[k] = input_of_frame(f0 + k);
-  // the phase-split games read the window through this lane's view of each input
-  // (ex_game: the lane's player's byte), taken once as an input enters the window
-  [[maybe_unused]] uint32_t lin[CD + 1];
+  // the phase-split games read the window decoded (games.hpp ExGame::Dec), each
+  // input once, as it enters the window
+  [[maybe_unused]] DecOf<G> dec[CD + 1];
   if constexpr (G::kHasPrep) {
 #pragma unroll
-    for (int k = 0; k <= CD; ++k) lin[k] = G::lane_input(win[k], lane);
+    for (int k = 0; k <= CD; ++k) dec[k] = G::decode(win[k], lane);
   }
   CS fsw[NF];  // SyncTest first-seen checksums of frames f0+1 .. f0+CD-1
 #pragma unroll
@@ -468,7 +478,7 @@ __global__ void __launch_bounds__(256) steady_kernel(const RunParams p) {
     constexpr bool kInRange = decltype(in_range_tag)::value;
     [[maybe_unused]] PrepOf<G, CD + 1> prep;
     if constexpr (G::kHasPrep && !kExp)  // the tick's rotation chain and thrust first (games.hpp)
-      G::template prepare<kInRange, CD + 1>(w, lin, prep, &p.counters[1]);
+      G::template prepare<kInRange, CD + 1>(w, dec, prep, &p.counters[1]);
 #pragma unroll
     for (int k = 0; k <= CD; ++k) {
       const int f = f0 + k;
@@ -543,8 +553,8 @@ __global__ void __launch_bounds__(256) steady_kernel(const RunParams p) {
     win[CD] = next_last;
     if constexpr (G::kHasPrep) {
 #pragma unroll
-      for (int k = 0; k < CD; ++k) lin[k] = lin[k + 1];
-      lin[CD] = G::lane_input(next_last, lane);
+      for (int k = 0; k < CD; ++k) dec[k] = dec[k + 1];
+      dec[CD] = G::decode(next_last, lane);
     }
     newin = newin_next;
 #pragma unroll
