@@ -379,15 +379,27 @@ def bench_p2p(args):
         state = 4 * 5 * P
         bytes_rank = (adv / world * P + saves / world * (state + 6) + loads / world * state
                       + S * args.steps * 8)
-        if args.fanout:  # per branch frame: its cell + checksum stored; per session-tick: base cell load,
-            # 16 branch states stored, per select: the selected cells read back
+        generic_fan = os.environ.get("RB_FANOUT_GENERIC", "0") not in ("", "0")
+        if args.fanout and generic_fan:  # fanout_kernel: per branch frame its cell + checksum stored and its
+            # inputs; per session-tick the base cell load and 16 branch states stored; per select the
+            # selected cells read back
             bytes_rank += branch / world * (state + 2 + P) + S * args.steps * state * 17 + selects / world * state
+        elif args.fanout:  # fanout_indep_kernel: the players not speculated on are simulated once per
+            # session, so per presimulated frame 16 x (the speculated player's cell part + checksum + input)
+            # + (P - 1) x (a player's cell part + input); per session-tick the base cell load and the final
+            # states (16 speculated + P - 1 others); per select the selected cells read back
+            ps = state // P
+            frames = branch / world / 16
+            bytes_rank += (frames * (16 * (ps + 2 + 1) + (P - 1) * (ps + 1)) + S * args.steps * (state + (16 + P - 1) * ps)
+                           + selects / world * state)
         avg_kernel_s = kernel_ms / 1e3 / max(1, launches)
         cfg_key = (f"p2p ex_game P={P} W={W} d={args.input_delay} rd={args.remote_delay} lag={lo},{hi} S={S}"
                    + (" sparse" if args.sparse_saving else "") + (" fanout" if args.fanout else "")
                    + (" wire" if args.wire else ""))
         roofline = roofline_block(bytes_rank / max(1, launches), avg_kernel_s, args.steps / max(1, launches), launches,
-                                  f"p2p_kernel<ExGame<{P},true>>" + (" + fanout_kernel (per tick)" if args.fanout
+                                  f"p2p_kernel<ExGame<{P},true>>" + ((" + fanout_kernel (per tick)" if generic_fan
+                                                                      else " + fanout_indep_kernel (per tick)")
+                                                                     if args.fanout
                                                                      else " (fused P2P ticks)"),
                                   pmc_profile(cfg_key), "algorithmic: cells loaded/saved, inputs, deliveries")
         line = {

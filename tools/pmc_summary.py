@@ -69,7 +69,7 @@ def main():
                 v = vals[1:] if len(vals) > 1 else vals
                 ent[c] = sum(v) / len(v)
     # the dominant kernel: the fused steady / P2P kernel of the bench line
-    steady = [k for k in summary["kernels"] if "steady_kernel" in k or "p2p_kernel" in k or "fanout_kernel" in k]
+    steady = [k for k in summary["kernels"] if "steady_kernel" in k or "p2p_kernel" in k or "fanout" in k]
     if steady:
         k = max(steady, key=lambda n: summary["kernels"][n].get("total_ns", 0.0))
         e = summary["kernels"][k]
@@ -80,7 +80,7 @@ def main():
             summary["hbm_bytes_per_tick"] = b / tpl
             # the speculative fan-out runs one p2p_kernel and one fanout_kernel per tick: a tick's
             # traffic is both dispatches'
-            if "fanout_kernel" in k:
+            if "fanout" in k:
                 for o in steady:
                     if "p2p_kernel" in o and "FETCH_SIZE" in summary["kernels"][o]:
                         eo = summary["kernels"][o]
