@@ -704,7 +704,8 @@ struct GameOpsT final : GameOps {
   hipError_t launch_fanout(const FanParams& p, int block, hipStream_t st) const override {
     if constexpr (kFanout && IndepPlayers<G>::value) {  // the players the fan-out does not speculate on, once
       if (!p.fan_generic) {
-        const int grid = (p.Spad * kIndepLanes + block - 1) / block;
+        const int waves = (p.S + indep_sessions_per_wave<G>() - 1) / indep_sessions_per_wave<G>();
+        const int grid = (waves * 64 + block - 1) / block;
         hipLaunchKernelGGL(fanout_indep_kernel<G>, dim3(grid), dim3(block), 0, st, p);
         return hipGetLastError();
       }

@@ -1252,13 +1252,23 @@ __global__ void __launch_bounds__(256) fanout_kernel(const FanParams p) {
 
 // The fan-out for games whose players move independently (G::kIndependentPlayers,
 // ex_game): the 16 branches differ only in the speculated player's lane, so a
-// session takes 32 lanes — lanes 0-15 the speculated player in branches 0-15,
-// lane 16 + h every other player h once — instead of 16 x L.  Cells and states
-// go to column s * 32 + lane of planes Spad * 32 wide (the spec buffers hold
-// Spad * 16 * L >= Spad * 32 columns), so a session's stores are one
-// contiguous run per plane; try_select reads that layout.  Each branch cell's
-// checksum is assembled from the branch lane's part and the sum of the other
-// players' parts.
+// session takes 16 + P - 1 lanes — 16 lanes for the speculated player in
+// branches 0-15, then one lane for every other player — instead of 16 x L, and
+// a wave holds 64 / (16 + P - 1) sessions (3 at P = 2..4: 89% of the lanes busy
+// at P = 4).  Cells and states go to column s * 32 + k (branch k of the
+// speculated player) or s * 32 + 16 + h (player h, one trajectory for all
+// branches) of planes Spad * 32 wide (the spec buffers hold Spad * 16 * L >=
+// Spad * 32 columns); try_select reads that layout.  Each branch cell's
+// checksum is assembled from the branch lane's part and the other players'
+// parts (lane shuffles within the session's lanes).
+template <class G>
+constexpr int indep_session_lanes() {
+  return kSpecBranches + G::kPlayers - 1;
+}
+template <class G>
+constexpr int indep_sessions_per_wave() {
+  return 64 / indep_session_lanes<G>();
+}
 template <class G>
 __global__ void __launch_bounds__(256) fanout_indep_kernel(const FanParams p) {
   using InRec = typename G::InRec;
@@ -1266,11 +1276,14 @@ __global__ void __launch_bounds__(256) fanout_indep_kernel(const FanParams p) {
   constexpr int NW = G::NWL;
   constexpr int L = G::kLanes;
   constexpr int P = G::kPlayers, IB = G::kInputBytes;
+  constexpr int LS = indep_session_lanes<G>(), SPW = indep_sessions_per_wave<G>();
   static_assert(IndepPlayers<G>::value && L > 1 && P <= kIndepLanes - kSpecBranches, "independent players, one per lane");
   const unsigned g = blockIdx.x * blockDim.x + threadIdx.x;
-  const unsigned s = g / kIndepLanes;
-  const int r = static_cast<int>(g % kIndepLanes);
-  if (s >= static_cast<unsigned>(p.S)) return;  // the session's 32 lanes leave together
+  const int wl = static_cast<int>(g % 64), j = wl / LS, r = wl % LS;
+  if (j >= SPW) return;  // the wave's spare lanes
+  const unsigned s = (g / 64) * SPW + static_cast<unsigned>(j);
+  if (s >= static_cast<unsigned>(p.S)) return;  // the session's lanes leave together
+  const int lane0 = j * LS;                     // the session's first lane in the wave
   const unsigned Spad = static_cast<unsigned>(p.Spad), Gpad = Spad * L;
   const unsigned Gs = Spad * kIndepLanes;  // spec plane width in this layout
   const int W = p.W;
@@ -1304,36 +1317,37 @@ __global__ void __launch_bounds__(256) fanout_indep_kernel(const FanParams p) {
   if (!valid) return;  // session-uniform
   const bool branch = r < kSpecBranches;
   const int k = branch ? r : 0;
-  const int h = branch ? rs : r - kSpecBranches;  // this lane's player
-  const bool active = branch || (h < P && h != rs);
-  const int hh = h < P ? h : 0;                   // an idle lane reads player 0's data and stores nothing
+  const int o = r - kSpecBranches;                        // the other players, in handle order, skipping rs
+  const int h = branch ? rs : (o < rs ? o : o + 1);       // this lane's player
   uint32_t w[NW];
-  load_words<NW>(p.snap + static_cast<unsigned>(base % W) * NW * Gpad, static_cast<int>(Gpad), static_cast<int>(s * L + hh), w);
-  const bool local = (p.local_mask >> hh) & 1u;
-  const int32_t la_h = qrow(QF_LAST_ADDED, hh);
-  const uint32_t pred = la_h == kNullFrame ? 0u : ring.get(la_h, hh, s);
-  const unsigned col = g;  // s * 32 + r
+  load_words<NW>(p.snap + static_cast<unsigned>(base % W) * NW * Gpad, static_cast<int>(Gpad), static_cast<int>(s * L + h), w);
+  const bool local = (p.local_mask >> h) & 1u;
+  const int32_t la_h = qrow(QF_LAST_ADDED, h);
+  const uint32_t pred = la_h == kNullFrame ? 0u : ring.get(la_h, h, s);
+  const unsigned col = s * kIndepLanes + static_cast<unsigned>(branch ? k : kSpecBranches + h);
   CS* __restrict__ cs = reinterpret_cast<CS*>(p.spec_cs);
   uint32_t frames = 0;
   for (int32_t f = base; f < cur; ++f) {
     if (f > base) {  // SaveGameState of frame f in every branch
-      Fl16 a = active ? G::fan_partial(w, hh) : Fl16{0u, 0u};
-      // the other players' parts: lanes 16-19 of the session are one DPP quad; their sum to every lane
-      uint32_t o1 = group_sum<4>(branch ? 0u : a.s1), o2 = group_sum<4>(branch ? 0u : a.s2);
-      o1 = static_cast<uint32_t>(__shfl(static_cast<int>(o1), kSpecBranches, kIndepLanes));
-      o2 = static_cast<uint32_t>(__shfl(static_cast<int>(o2), kSpecBranches, kIndepLanes));
+      const Fl16 a = G::fan_partial(w, h);
+      uint32_t o1 = 0u, o2 = 0u;  // the other players' parts, read from their lanes
+#pragma unroll
+      for (int q = 0; q < P - 1; ++q) {
+        o1 += static_cast<uint32_t>(__shfl(static_cast<int>(a.s1), lane0 + kSpecBranches + q, 64));
+        o2 += static_cast<uint32_t>(__shfl(static_cast<int>(a.s2), lane0 + kSpecBranches + q, 64));
+      }
       const unsigned slot = static_cast<unsigned>(f % W);
-      if (active) store_words<NW>(p.spec_cells + slot * NW * Gs, static_cast<int>(Gs), static_cast<int>(col), w);
+      store_words<NW>(p.spec_cells + slot * NW * Gs, static_cast<int>(Gs), static_cast<int>(col), w);
       if (branch) cs[(slot * Spad + s) * kSpecBranches + k] = G::fan_finish(Fl16{a.s1 + o1, a.s2 + o2}, f);
     }
     uint32_t v;
     if (branch) v = static_cast<uint32_t>(k);
-    else if (local || (la_h != kNullFrame && f <= la_h)) v = ring.get(f, hh, s);  // Confirmed
+    else if (local || (la_h != kNullFrame && f <= la_h)) v = ring.get(f, h, s);  // Confirmed
     else v = pred;  // repeat-last prediction (blank before the first input)
-    G::advance(w, static_cast<InRec>(static_cast<uint64_t>(v) << (8 * IB * hh)), hh, 0u, &p.counters[1]);
+    G::advance(w, static_cast<InRec>(static_cast<uint64_t>(v) << (8 * IB * h)), h, 0u, &p.counters[1]);
     ++frames;
   }
-  if (active) store_words<NW>(p.spec_state, static_cast<int>(Gs), static_cast<int>(col), w);
+  store_words<NW>(p.spec_state, static_cast<int>(Gs), static_cast<int>(col), w);
   if (r == 0) p.stats[ST_BRANCH * Spad + s] += static_cast<unsigned long long>(frames) * kSpecBranches;
 }
 
