@@ -470,6 +470,41 @@ def test_gpu_p2p_disconnect_matches_oracle_every_tick(gpu_available, case):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("sync_ticks", [False, True], ids=["async", "lockstep"])
+@pytest.mark.parametrize("P,mask", [(2, 0b01), (4, 0b0001)])
+def test_gpu_p2p_disconnects_between_fused_launches(gpu_available, monkeypatch, P, mask, sync_ticks):
+    # disconnect_player between multi-tick launches (the disconnect's rollback and
+    # the (zeroed, Disconnected) inputs then run inside fused launches where the
+    # sessions sit at different ticks, p2p.hpp kAsync): after every launch the last
+    # tick's request counts and every cell, state and queue equal the oracle's.
+    import torch
+    monkeypatch.setenv("RB_P2P_SYNC_TICKS", "1" if sync_ticks else "0")
+    W, d, rd, (lo, hi) = 8, 1, 1, (1, 5)
+    S, T, tpl = 150, 80, 11
+    inputs, upto, rin = synth_network(S, P, T, mask, rd, lo, hi)
+    sess, orc = gpu_pair(G.Game.EX_GAME, S, P, W, d, rd, mask, False)
+    remotes = [h for h in range(P) if not (mask >> h) & 1]
+    half = np.arange(S) % 2 == 0
+    disc = {30: [(remotes[-1], half)], 47: [(remotes[-1], ~half)]}
+    if len(remotes) > 1:
+        disc[55] = [(remotes[0], np.arange(S) % 3 == 0)]
+    cuts = sorted(set(list(range(0, T, tpl)) + list(disc) + [T]))
+    di, du, dr = (torch.from_numpy(a).cuda() for a in (inputs, upto, rin))
+    for t0, t1 in zip(cuts[:-1], cuts[1:]):
+        for hh, m in disc.get(t0, []):
+            sess.disconnect_player(hh, m)
+        ost, olf, ona, ons = drive_oracle(orc, mask, inputs, upto, rin, t1, t0=t0, disc=disc)[-1]
+        sess.run_ticks(di[t0:t1], du[t0:t1], dr)
+        st, lf, na, ns = sess.status()
+        np.testing.assert_array_equal(st, ost, err_msg=f"status, tick {t1 - 1}")
+        np.testing.assert_array_equal(lf, olf, err_msg=f"LoadGameState frame, tick {t1 - 1}")
+        np.testing.assert_array_equal(na, ona, err_msg=f"AdvanceFrame count, tick {t1 - 1}")
+        np.testing.assert_array_equal(ns, ons, err_msg=f"SaveGameState count, tick {t1 - 1}")
+        compare_state(sess, orc, t1 - 1)
+    assert sess.counters()[2] == 0
+
+
+@pytest.mark.gpu
 def test_gpu_disconnect_at_the_current_frame_asserts_like_reference(gpu_available):
     # The device side of test_oracle_disconnect_at_the_current_frame_asserts_like_reference.
     import torch
