@@ -672,7 +672,7 @@ struct GameOpsT final : GameOps {
   static hipError_t launch_p2p_as(const P2PParams& p, int grid, int block, hipStream_t st) {
     size_t lds = p2p_lds_bytes<G>(block);
     if constexpr (!kSpec && !kNet && p2p_lds_queue<G>()) {
-      if (p2p_lds_cells<G>(p.W)) {  // the snapshot ring in LDS (p2p_lds_cell_bytes)
+      if (p2p_lds_cells<G>(p.W, block)) {  // the snapshot ring in LDS (p2p_lds_cell_bytes)
         // lane-asynchronous ticks on the plain path unless the batch asked for lock-step ticks
         auto k = (!kSparse && !p.sync_ticks) ? p2p_kernel<G, kSpec, kSparse, kNet, true, !kSparse>
                                              : p2p_kernel<G, kSpec, kSparse, kNet, true, false>;

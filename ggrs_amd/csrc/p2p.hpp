@@ -347,9 +347,14 @@ constexpr size_t p2p_lds_cell_bytes(int block, int W) {
   return static_cast<size_t>(W) * (static_cast<size_t>(G::NWL) * 4 * block +
                                    (4 + sizeof(typename G::CS)) * static_cast<size_t>(block / G::kLanes));
 }
+// ... when the queue and the cells of a block fit half of a CU's 160 KiB (two
+// blocks per CU): ex_game's 40 B cells do (79 KiB at 256 threads, W = 8), the
+// brawler's 8 KiB cells do not and stay in HBM.
+constexpr size_t kLdsPerBlockMax = 80 * 1024;
 template <class G>
-constexpr bool p2p_lds_cells(int W) {
-  return p2p_lds_queue<G>() && W <= kLdsCellsMaxW;
+constexpr bool p2p_lds_cells(int W, int block) {
+  return p2p_lds_queue<G>() && W <= kLdsCellsMaxW &&
+         p2p_lds_bytes<G>(block) + p2p_lds_cell_bytes<G>(block, W) <= kLdsPerBlockMax;
 }
 
 // input_queue.rs:167-204 add_input_by_frame

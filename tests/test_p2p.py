@@ -247,6 +247,9 @@ CASES = [  # game, P, W, d, rd, local_mask, sparse, lag range
     (G.Game.STUB_ENUM, 2, 6, 0, 2, 0b10, True, (0, 5)),
     # W > 8: the snapshot ring stays in HBM (the LDS ring holds at most 8 cells)
     (G.Game.EX_GAME, 2, 12, 1, 1, 0b01, False, (1, 9)),
+    # the brawler: one wave per session, 8 KiB cells (too big for the LDS ring: HBM cells)
+    (G.Game.BRAWLER, 2, 8, 1, 1, 0b01, False, (1, 4)),
+    (G.Game.BRAWLER, 2, 6, 0, 2, 0b10, True, (0, 5)),
     (G.Game.EX_GAME, 3, 10, 0, 2, 0b001, True, (1, 7)),
 ]
 
