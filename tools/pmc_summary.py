@@ -78,11 +78,12 @@ def main():
             b = (2 * e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024
             summary["hbm_bytes_per_launch"] = b
             summary["hbm_bytes_per_tick"] = b / tpl
-            # the speculative fan-out runs one p2p_kernel and one fanout_kernel per tick: a tick's
-            # traffic is both dispatches'
-            if "fanout" in k:
+            # the speculative fan-out runs one p2p_kernel and one fan-out kernel per tick: a tick's
+            # traffic is both dispatches' (whichever of the two takes longer)
+            fan = [o for o in steady if "fanout" in o]
+            if fan and any("p2p_kernel" in o for o in steady):
                 for o in steady:
-                    if "p2p_kernel" in o and "FETCH_SIZE" in summary["kernels"][o]:
+                    if o != k and ("fanout" in o or "p2p_kernel" in o) and "FETCH_SIZE" in summary["kernels"][o]:
                         eo = summary["kernels"][o]
                         summary["hbm_bytes_per_tick"] += (2 * eo["FETCH_SIZE"] + eo["WRITE_SIZE"]) * 1024 / tpl
                         summary["tick_kernels"] = [k, o]
