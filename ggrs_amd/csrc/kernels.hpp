@@ -672,7 +672,9 @@ struct GameOpsT final : GameOps {
   static hipError_t launch_p2p_as(const P2PParams& p, int grid, int block, hipStream_t st) {
     size_t lds = p2p_lds_bytes<G>(block);
     if constexpr (!kSpec && !kNet && p2p_lds_queue<G>()) {
-      if (p2p_lds_cells<G>(p.W, block)) {  // the snapshot ring in LDS (p2p_lds_cell_bytes)
+      // the snapshot ring in LDS (p2p_lds_cell_bytes) for launches of many ticks: it is copied in and
+      // written back whole, which short launches (the wire path's one tick per launch) do not repay
+      if (p2p_lds_cells<G>(p.W, block) && p.T >= kLdsCellsMinTicks) {
         // lane-asynchronous ticks on the plain path unless the batch asked for lock-step ticks
         auto k = (!kSparse && !p.sync_ticks) ? p2p_kernel<G, kSpec, kSparse, kNet, true, !kSparse>
                                              : p2p_kernel<G, kSpec, kSparse, kNet, true, false>;

@@ -351,6 +351,13 @@ constexpr size_t p2p_lds_cell_bytes(int block, int W) {
 // blocks per CU): ex_game's 40 B cells do (79 KiB at 256 threads, W = 8), the
 // brawler's 8 KiB cells do not and stay in HBM.
 constexpr size_t kLdsPerBlockMax = 80 * 1024;
+#ifndef RB_LDS_CELLS_MIN_TICKS
+#define RB_LDS_CELLS_MIN_TICKS 24
+#endif
+// launches of fewer ticks keep the cells in HBM (and lock-step ticks): copying the
+// ring in and out costs more than it saves below about 24 ticks (measured: HBM
+// cells 4.8 us per tick at 16 ticks per launch, LDS cells 4.1 at 32)
+constexpr int kLdsCellsMinTicks = RB_LDS_CELLS_MIN_TICKS;
 template <class G>
 constexpr bool p2p_lds_cells(int W, int block) {
   return p2p_lds_queue<G>() && W <= kLdsCellsMaxW &&

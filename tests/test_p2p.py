@@ -483,7 +483,7 @@ def test_gpu_p2p_disconnects_between_fused_launches(gpu_available, monkeypatch, 
     import torch
     monkeypatch.setenv("RB_P2P_SYNC_TICKS", "1" if sync_ticks else "0")
     W, d, rd, (lo, hi) = 8, 1, 1, (1, 5)
-    S, T, tpl = 150, 80, 11
+    S, T, tpl = 150, 80, 26  # launches of >= 24 ticks run the lane-asynchronous kernel, shorter ones lock-step
     inputs, upto, rin = synth_network(S, P, T, mask, rd, lo, hi)
     sess, orc = gpu_pair(G.Game.EX_GAME, S, P, W, d, rd, mask, False)
     remotes = [h for h in range(P) if not (mask >> h) & 1]
