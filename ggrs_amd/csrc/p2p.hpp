@@ -473,8 +473,9 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
   if (s >= static_cast<unsigned>(p.S)) return;  // whole lane groups leave together
   // A session that hit a reference assert stays stopped (the reference
   // process would have aborted): it reports RB_PANIC from then on and its
-  // state, cells and queues stay as the panic left them.
-  if (p.status[s] == kP2PStatusPanic) return;
+  // state, cells and queues stay as the panic left them.  (Checked once the
+  // session's state loads are issued, so they do not wait for this one.)
+  const bool panicked = p.status[s] == kP2PStatusPanic;
   const unsigned Spad = static_cast<unsigned>(p.Spad), Gpad = Spad * L;
   const unsigned slot_words = static_cast<unsigned>(NW) * Gpad;
   const int W = p.W;
@@ -531,6 +532,15 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
   auto conn_of = [&](int j) __attribute__((always_inline)) { return q[j].disc ? INT32_MAX : q[j].conn_last; };
   uint32_t w[NW];
   load_words<NW>(p.live, static_cast<int>(Gpad), static_cast<int>(g), w);
+  // the fan-out's branch metadata (written between launches), with the state loads
+  [[maybe_unused]] int32_t sm_valid = 0, sm_end = 0, sm_base = 0, sm_player = 0;
+  if constexpr (kSpec) {
+    sm_valid = p.spec_meta[SM_VALID * Spad + s];
+    sm_end = p.spec_meta[SM_END * Spad + s];
+    sm_base = p.spec_meta[SM_BASE * Spad + s];
+    sm_player = p.spec_meta[SM_PLAYER * Spad + s];
+  }
+  if (panicked) return;
   // LDS queue: the HBM frames this launch can read.  Reads are of frames
   // >= cur - W (adjust_gamestate checks that before it advances) up to the
   // last added one, or of the last added frame itself (predictions and the
@@ -688,9 +698,9 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
   // bookkeeping runs as in adjust (dry), the cells and the state are copied.
   auto try_select = [&](int32_t first_incorrect, int32_t min_confirmed) __attribute__((always_inline)) -> bool {
     if (any_disc || disc_frame != kNullFrame) return false;  // the branches assumed everybody connected
-    if (!p.spec_meta[SM_VALID * Spad + s] || p.spec_meta[SM_END * Spad + s] != cur) return false;
-    const int32_t base = p.spec_meta[SM_BASE * Spad + s];
-    const int rs = p.spec_meta[SM_PLAYER * Spad + s];
+    if (!sm_valid || sm_end != cur) return false;
+    const int32_t base = sm_base;
+    const int rs = sm_player;
     if (first_incorrect != base || base + W <= cur) return false;
     // every mispredicting player must be the speculated one; its confirmed run from base must be one value
     bool ok = true;
