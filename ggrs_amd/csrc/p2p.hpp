@@ -870,12 +870,18 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
   // The tick's opening, through the PredictionThreshold decision: 0 = the
   // session stopped on a panic, 1 = the tick is over (Err(PredictionThreshold)),
   // 2 = rollback_and_save, add_local_input and the new frame follow.
+  // The next tick's deliveries are prefetched, except by the fan-out's P2P
+  // launches, which are always of one tick (the fan-out runs between ticks):
+  // there they would only hold registers.
+  constexpr bool kPrefetch = !kSpec;
   auto tick_begin = [&](int t) __attribute__((always_inline)) -> int {
     const int tn = t + 1 < p.T ? t + 1 : t;
+    if constexpr (kPrefetch) {
 #pragma unroll
-    for (int j = 0; j < PPL; ++j) {
-      up_n[j] = load_upto(tn, j);
-      lin_n[j] = load_local(tn, j);
+      for (int j = 0; j < PPL; ++j) {
+        up_n[j] = load_upto(tn, j);
+        lin_n[j] = load_local(tn, j);
+      }
     }
     status = kP2PStatusOk;
     load_frame = kNullFrame;
@@ -899,11 +905,13 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
         }
       }
     }
+    if constexpr (kPrefetch) {
 #pragma unroll
-    for (int j = 0; j < PPL; ++j) {
-      const int32_t f = remote_start(j);
+      for (int j = 0; j < PPL; ++j) {
+        const int32_t f = remote_start(j);
 #pragma unroll
-      for (int k = 0; k < kPre; ++k) rv_n[j][k] = load_remote(j, f + k);
+        for (int k = 0; k < kPre; ++k) rv_n[j][k] = load_remote(j, f + k);
+      }
     }
     {  // input_queue.rs:181 assert!(self.length <= INPUT_QUEUE_LENGTH) fired during the poll.  No
       // branch here: the panic status is picked up by the panic check after the threshold decision
@@ -1026,12 +1034,14 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     }
   };
   auto tick_rotate = [&]() __attribute__((always_inline)) {  // the prefetched deliveries become the next tick's
+    if constexpr (kPrefetch) {
 #pragma unroll
-    for (int j = 0; j < PPL; ++j) {
-      up[j] = up_n[j];
-      lin[j] = lin_n[j];
+      for (int j = 0; j < PPL; ++j) {
+        up[j] = up_n[j];
+        lin[j] = lin_n[j];
 #pragma unroll
-      for (int k = 0; k < kPre; ++k) rv[j][k] = rv_n[j][k];
+        for (int k = 0; k < kPre; ++k) rv[j][k] = rv_n[j][k];
+      }
     }
   };
   auto tick = [&](int t) __attribute__((always_inline)) -> bool {
