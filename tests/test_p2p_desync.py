@@ -219,3 +219,34 @@ def test_gpu_input_queue_overflow_panics_and_the_panic_sticks(gpu_available):
     assert g.counters()[2] == victims.sum()  # each panicked session counted once
     live = ~victims
     np.testing.assert_array_equal(g.read_live()[live], orc.read_live()[0][live])
+
+
+@pytest.mark.gpu
+def test_gpu_queue_overflow_panic_inside_fused_launches(gpu_available):
+    # The same overflow, tripped inside launches of 30 ticks (lane-asynchronous
+    # ticks, p2p.hpp kAsync): the victims stop at the tick the oracle panics,
+    # the other sessions run on and equal the oracle after every launch.
+    import torch
+    S, T, d, tpl = 64, 60, 1, 30
+    inputs, (upto, rin), _ = networks(S, T, d, (1, 2))
+    far = T + 200
+    rin = np.concatenate([rin, np.zeros((far - rin.shape[0], P, S), rin.dtype)])
+    upto = upto.copy()
+    victims = np.zeros(S, bool)
+    victims[[2, 9, 33]] = True
+    upto[20:, 1, victims] = np.arange(20, T)[:, None] + 150
+    orc = oracle_peer(MASK_A, S, d, 0)
+    g = gpu_peer(MASK_A, S, d, 0)
+    dev = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()
+    di, du, dr = dev(inputs), dev(upto), dev(rin)
+    live = ~victims
+    for t0 in range(0, T, tpl):
+        g.run_ticks(di[t0:t0 + tpl], du[t0:t0 + tpl], dr)
+        for t in range(t0, t0 + tpl):
+            ost = oracle_tick(orc, MASK_A, inputs, (upto, rin), t)[0]
+        st = g.status()[0]
+        np.testing.assert_array_equal(st, np.where(ost == ORC_PANIC, RB_PANIC, ost), err_msg=f"tick {t0 + tpl - 1}")
+        assert (st[victims] == RB_PANIC).all() and (st[live] == 0).all()
+        np.testing.assert_array_equal(g.frames()[0], orc.frames()[0])
+        np.testing.assert_array_equal(g.read_live()[live], orc.read_live()[0][live])
+    assert g.counters()[2] == victims.sum()
