@@ -1,3 +1,7 @@
+#!/bin/bash
+# Lane-asynchronous P2P ticks, experiment run (GPU box): loop iterations per wave
+# (tools/p2p_iters.py on a `tools/mkvar.sh p2pexp4 -DRB_P2P_EXP=4` build) at three
+# lags, then the instruction mix of lock-step vs asynchronous ticks.
 export TMPDIR=/tmp
 GGRS_AMD_LIB=$PWD/ggrs_amd/var/lib_p2pexp4.so timeout -k 10 120 python -u tools/p2p_iters.py > gpurun_out/iters.log 2>&1 && 
 LAG=0,0 GGRS_AMD_LIB=$PWD/ggrs_amd/var/lib_p2pexp4.so timeout -k 10 120 python -u tools/p2p_iters.py >> gpurun_out/iters.log 2>&1 &&
