@@ -116,6 +116,11 @@ def launch_ranks(n):
 
 
 def cpu_baseline(args, P):
+    """The reference CPU path timed on this box's host cores: the C++
+    line-faithful restatement with the reference's allocation pattern (kind
+    "port"), and for ex_game next to it the optimized CPU loop SURVEY 8(d)
+    asks for ("optimized": oracle/soa_baseline.cpp, same arithmetic and
+    checksums, no per-request allocation, cache-blocked sessions)."""
     from oracle import oracle as O
     threads = cpu_threads()
     S, warm, ticks = args.cpu_sessions, 16, args.cpu_ticks
@@ -126,10 +131,23 @@ def cpu_baseline(args, P):
         ticks = 256 if args.game == "brawler" else 384
     secs, nerr = fn(P, args.check_distance, args.input_delay, args.max_prediction, S, warm, ticks, threads, args.seed)
     sf = S * ticks * (args.check_distance + 1)
-    return {"value": sf / secs, "unit": "session-frames/s", **cpu_info(threads), "kind": "port",
-            "sample": f"{S} {args.game} sessions x {ticks} steady-state ticks ({sf} session-frames) of the C++ "
-                      f"line-faithful restatement (reference allocation pattern), {threads} host threads "
-                      f"(every core this job may use), {secs:.2f} s wall, {nerr} errors"}
+    out = {"value": sf / secs, "unit": "session-frames/s", **cpu_info(threads), "kind": "port",
+           "sample": f"{S} {args.game} sessions x {ticks} steady-state ticks ({sf} session-frames) of the C++ "
+                     f"line-faithful restatement (reference allocation pattern), {threads} host threads "
+                     f"(every core this job may use), {secs:.2f} s wall, {nerr} errors"}
+    if args.game == "ex_game":
+        oticks = 512
+        osecs, oerr = O.bench_exgame_soa(P, args.check_distance, args.input_delay, args.max_prediction, S, warm,
+                                         oticks, threads, args.seed)
+        osf = S * oticks * (args.check_distance + 1)
+        out["optimized"] = {
+            "value": osf / osecs, "unit": "session-frames/s", **cpu_info(threads), "kind": "optimized",
+            "sample": f"{S} ex_game sessions x {oticks} steady-state ticks ({osf} session-frames), same inputs, "
+                      f"State::advance arithmetic (glibc sinf/cosf) and fletcher16 as the port; per-session "
+                      f"snapshot rings in flat arrays, no per-request allocation, closed-form fletcher16, "
+                      f"256-session blocks kept in cache across ticks (oracle/soa_baseline.cpp), {threads} host "
+                      f"threads, {osecs:.2f} s wall, {oerr} errors"}
+    return out
 
 
 def measured_copy_gbps(dev, nbytes=1 << 30, iters=10):
@@ -169,36 +187,54 @@ def pmc_profile(cfg_key):
     return best
 
 
+STORE_CEILING_FILE = os.path.join(ROOT, "profiles", "r02_calib_write.json")
+
+
+def store_ceiling_gbps():
+    """The calibrated store-only ceiling of the brawler's SaveGameState pattern
+    (tools/calib_write.hip, profiles/r02_calib_write.json: 5.9 TB/s), or None."""
+    try:
+        return float(json.load(open(STORE_CEILING_FILE))["store_only_GBps"])
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def roofline_block(bytes_per_launch, avg_kernel_s, ticks_per_launch, launches, kernel, prof, model):
     """The bench line's roofline object.  `achieved`/`frac` are the contract's:
     algorithmic bytes per launch (`model` says which bytes) over the measured
-    average launch time, against the 8 TB/s spec peak.  Next to them, from the
-    committed PMC profile of the same configuration: the HBM bytes the counters
-    saw (`traffic`, `traffic_frac`), the VALU issue-slot fraction, and the
-    resource that actually limits the kernel (`limiter`)."""
+    average launch time, against the 8 TB/s spec peak (`frac_basis`).  Next to
+    them, from the committed PMC profile of the same configuration: the HBM
+    bytes the counters saw (`traffic`) and their fraction of peak (`dram_frac`),
+    the VALU issue-slot fraction, and `bound` = what actually limits the
+    kernel, decided from those counters: "hbm" when the DRAM-side traffic is
+    above 0.7 of peak, "valu" when the VALU issue slots are above 0.7 busy,
+    "latency" (dependent chains at low occupancy) otherwise; "unprofiled"
+    when no PMC profile of this configuration is committed."""
     achieved = bytes_per_launch / avg_kernel_s / 1e9
-    r = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-         "traffic": None, "algorithmic_bytes_per_launch": bytes_per_launch, "bytes_model": model,
+    r = {"bound": "unprofiled", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": achieved / HBM_PEAK_GBS, "frac_basis": "algorithmic bytes / kernel time / 8 TB/s HBM spec",
+         "traffic": None, "dram_frac": None, "algorithmic_bytes_per_launch": bytes_per_launch, "bytes_model": model,
          "kernel_avg_us": avg_kernel_s * 1e6, "ticks_per_launch": ticks_per_launch, "launches_timed": launches,
          "kernel": kernel}
     if prof:
         traffic = prof["hbm_bytes_per_tick"] * ticks_per_launch
         r["traffic"] = traffic
-        r["traffic_frac"] = traffic / avg_kernel_s / 1e9 / HBM_PEAK_GBS
+        r["dram_frac"] = r["traffic_frac"] = traffic / avg_kernel_s / 1e9 / HBM_PEAK_GBS
         r["pmc_profile"] = prof["file"]
         iss = prof.get("issue")
         if iss:
             r["valu"] = {k: iss[k] for k in ("valu_insts_per_wave", "valu_issue_frac", "issue_stall_frac",
                                               "waves_per_simd", "waves_dispatched_per_simd", "clock_GHz_sq",
                                               "l2_hit") if k in iss}
-            if r["traffic_frac"] > 0.7:
-                r["limiter"] = "hbm bandwidth"
+            if r["dram_frac"] > 0.7:
+                r["bound"], r["limiter"] = "hbm", "hbm bandwidth"
             elif iss["valu_issue_frac"] > 0.7:
-                r["limiter"] = "valu issue"
+                r["bound"], r["limiter"] = "valu", "valu issue"
             else:
+                r["bound"] = "latency"
                 r["limiter"] = (f"dependency latency: {iss['waves_per_simd']:.1f} waves resident per SIMD, "
                                 f"{iss['valu_issue_frac']:.2f} of VALU issue slots, HBM traffic "
-                                f"{r['traffic_frac']:.2f} of peak")
+                                f"{r['dram_frac']:.2f} of peak")
     return r
 
 
@@ -461,6 +497,9 @@ def main():
                     help="ticks between RCCL all-gathers of desync reports (N>1); 0 = never")
     ap.add_argument("--ticks-per-launch", type=int, default=50,
                     help="steady-state ticks fused into one steady_kernel launch (rb_run_ticks call)")
+    ap.add_argument("--realtime-ticks", type=int, default=64,
+                    help="after the timed region, this many ticks of one rb_run_ticks call each (live play, "
+                         "inputs arriving per tick): the line's realtime / headroom_60hz fields; 0 = skip")
     ap.add_argument("--game", choices=["ex_game", "brawler"], default="ex_game",
                     help="ex_game = BASELINE configs[1] (default); brawler = configs[2]")
     ap.add_argument("--cpu-sessions", type=int, default=None)
@@ -522,7 +561,8 @@ def main():
     # always run untimed, before the W requested warmup ticks, so the timed region is steady state
     # and the warmup has run the fused steady kernel at least once.
     warm = cd + 1 + args.warmup
-    T = warm + args.steps
+    RT = args.realtime_ticks  # one-tick-per-call ticks after the timed region (the 60 Hz serving path)
+    T = warm + args.steps + RT
     # This rank's shard: global sessions [rank*S, (rank+1)*S); inputs keyed by global id.  With
     # N > 1 the batch also holds A audit replicas: the first A sessions of rank (r+1) % N.
     lo, hi = shard.shard_range(rank, world, S * world)
@@ -547,23 +587,30 @@ def main():
     audit_bad = torch.zeros((), dtype=torch.int64, device=dev)  # DesyncDetected: owner vs replica checksums
     gathers = [0]
 
-    def chunks(t0, t1):
+    def chunks(t0, t1, final_report=False):
         """Ticks [t0, t1) as native multi-tick calls of at most --ticks-per-launch
         ticks (one steady_kernel launch each once past the first cd+1 ticks),
         split further at desync-report points: (input slice, steady, report after).
-        SyncTest's current frame after t ticks is t, so the split is known up
-        front and the slices are views made before the timed region."""
+        With N > 1 a report is all-gathered every --report-interval ticks and,
+        with final_report, after the last tick (so every timed region runs the
+        collective at least once).  SyncTest's current frame after t ticks is
+        t, so the split is known up front and the slices are views made before
+        the timed region."""
         out, t = [], t0
+        every = world > 1 and args.report_interval
         while t < t1:
             n = min(t1 - t, args.ticks_per_launch)
             steady = t > cd
             if not steady:  # start-up ticks: per-tick launches, then align the steady chunks
                 n = min(n, cd + 1 - t)
-            if world > 1 and args.report_interval:
+            if every:
                 n = min(n, args.report_interval - t % args.report_interval)
             t += n
-            out.append((dinputs[t - n:t], steady, world > 1 and args.report_interval and t % args.report_interval == 0))
+            report = world > 1 and ((every and t % args.report_interval == 0) or (final_report and t == t1))
+            out.append((dinputs[t - n:t], steady, report))
         return out
+
+    gather_ev = []  # HIP event pairs around each all-gather (torch's current stream = the batch stream)
 
     def run(plan):
         steady_launches = 0
@@ -572,14 +619,18 @@ def main():
             steady_launches += steady
             if report:
                 f = sess.current_frame() - 1
-                sess.export_checksum_report(f, reports.data_ptr())
+                sess.export_checksum_report(f, reports)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
                 gathered = shard.gather_reports(reports)  # RCCL all-gather of desync reports
+                e1.record()
+                gather_ev.append((e0, e1))
                 desyncs.add_(shard.count_desynced(gathered, world, S, A))  # mismatch_frame != NULL_FRAME
                 audit_bad.add_(shard.audit_compare(gathered, world, S, A)[0])  # checksum of owner != replica
                 gathers[0] += 1
         return steady_launches
 
-    timed_plan = chunks(warm, T)
+    timed_plan = chunks(warm, warm + args.steps, final_report=True)
     with torch.cuda.stream(stream):
         run(chunks(0, warm))
         torch.cuda.synchronize()
@@ -596,6 +647,25 @@ def main():
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
         kernel_ms, timed_ticks = sess.profile_take()  # HIP events around every steady_kernel launch
+        gather_ms = [a.elapsed_time(b) for a, b in gather_ev]
+        # The 60 Hz serving path, after (outside) the timed region: inputs arrive one tick at a
+        # time (ex_game_synctest.rs:50-61), so each tick is its own call and launch.
+        rt = None
+        if RT:
+            t_rt = warm + args.steps
+            sess.profile_take()
+            torch.cuda.synchronize()
+            r0 = time.perf_counter()
+            for k in range(RT):
+                sess.run_ticks(dinputs[t_rt + k:t_rt + k + 1])
+            torch.cuda.synchronize()
+            rt_wall = time.perf_counter() - r0
+            rt_kernel_ms, rt_ticks = sess.profile_take()
+            rt = {"ticks": RT, "ticks_per_call": 1, "wall_us_per_tick": rt_wall / RT * 1e6,
+                  "kernel_us_per_tick": rt_kernel_ms * 1e3 / max(1, rt_ticks),
+                  "max_ticks_per_s": RT / rt_wall, "headroom_60hz": RT / rt_wall / 60.0,
+                  "note": "one tick per rb_run_ticks call (live play), all sessions of this GPU; headroom = "
+                          "sustainable ticks/s / 60"}
 
     nfail = int((sess.mismatches()[:S] != G.NULL_FRAME).sum())  # owned sessions only
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -618,21 +688,41 @@ def main():
         # word implicit); brawler 256 entities x 8 i32
         nw = 256 * 8 if brawler else 5 * P
         bpt = algorithmic_bytes_per_session_tick(P, cd, nw=nw, cs_bytes=2, in_bytes=1)
-        if brawler:
+        tpl = args.ticks_per_launch
+        if brawler and tpl > 1:
             # HBM-required bytes: the LoadGameState of a tick re-reads the cell the same lanes
-            # saved one tick earlier (an L2 hit), so only the saves must reach HBM
+            # saved one tick earlier in the same launch, so only the saves must reach HBM
             bpt -= 4 * nw
-            model = "HBM-required: cd saves x 8 KiB + checksums + inputs (the load re-reads an L2-hot cell)"
+            model = ("HBM-required: cd saves x 8 KiB + checksums + inputs (the load re-reads the cell the "
+                     "same wave saved one tick earlier in this launch)")
+        elif brawler:
+            model = ("algorithmic (SURVEY 8d): 1 load + cd saves x 8 KiB, checksums, inputs, status; one tick "
+                     "per launch, so the loaded cell (saved a launch and 3.5 GiB of stores earlier) streams "
+                     "from DRAM")
         else:
             model = "algorithmic (SURVEY 8d): 1 load + cd saves x 40 B, checksums, inputs, status"
         bytes_per_launch = bpt * (S + A) * ticks_per_launch  # the kernel runs the audit replicas too
-        cfg_key = f"{args.game} P={P} cd={cd} W={args.max_prediction} d={args.input_delay} S={S}"
+        cfg_key = f"{args.game} P={P} cd={cd} W={args.max_prediction} d={args.input_delay} S={S}" + (
+            f" tpl={tpl}" if tpl != 50 else "")
         roofline = roofline_block(bytes_per_launch, avg_kernel_s, ticks_per_launch, launches,
                                   (f"steady_kernel<Brawler<{P}>,{cd}>" if brawler else
-                                   f"steady_kernel<ExGame<{P},true>,{cd}>") + " (fused steady-state ticks)",
+                                   f"steady_kernel<ExGame<{P},true>,{cd}>") +
+                                  (" (fused steady-state ticks)" if tpl > 1 else " (one tick per launch)"),
                                   pmc_profile(cfg_key), model)
         roofline["algorithmic_bytes_per_session_tick"] = bpt
         roofline["measured_copy_GBps"] = measured_copy_gbps(dev)
+        if brawler:
+            ceil = store_ceiling_gbps()
+            roofline["store_ceiling_GBps"] = ceil
+            roofline["frac_of_store_ceiling"] = roofline["achieved"] / ceil if ceil else None
+            if tpl > 1 and ceil and roofline["achieved"] > ceil:
+                # a wave keeps its session for all the launch's ticks, and only about 3 waves per SIMD are
+                # resident: the ~3k sessions in flight rewrite their 64 KiB rings (~200 MB) inside the 256 MiB
+                # Infinity Cache, so more bytes are saved per second than DRAM can take
+                roofline["bound"] = "infinity-cache"
+                roofline["limiter"] = ("Infinity-Cache assisted (time-skewed sessions): the saves of the sessions "
+                                       "in flight are absorbed by the 256 MiB MALL; above the "
+                                       f"{ceil:.0f} GB/s DRAM store ceiling, so not an HBM figure")
         line = {
             "metric": METRIC,
             "value": value,
@@ -663,11 +753,18 @@ def main():
                 "mismatched_sessions": int(bad.item()),
                 "desync_reports": ({"ranks": ranks_seen, "backend": backend, "gathers": gathers[0],
                                     "interval_ticks": args.report_interval,
+                                    "allgather_ms": gather_ms, "allgather_bytes_per_rank": (S + A) * 24,
                                     "mismatch_rows_seen": int(desyncs.item()),
                                     "audit_sessions_per_rank": A, "audit_compared": A * world * gathers[0],
                                     "audit_desynced": int(audit_bad.item())} if world > 1 else None),
             },
             "roofline": roofline,
+            "realtime": rt,
+            "headroom_60hz": {"fused": args.steps / elapsed / 60.0,
+                              "one_tick_per_call": rt["headroom_60hz"] if rt else None,
+                              "note": "sustainable ticks/s of this GPU's sessions / 60: fused = the timed "
+                                      "region (inputs known ahead, a SyncTest replay), one_tick_per_call = "
+                                      "live play (realtime block)"},
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -98,6 +98,7 @@ SIGNATURES = [
     ("rb_destroy", None, [_P]),
     ("rb_last_error", ctypes.c_char_p, [_P]),
     ("rb_set_stream", _I32, [_P, _P]),
+    ("rb_get_stream", _P, [_P]),
     ("rb_add_local_input", _I32, [_P, _I32, _P, _I32]),
     ("rb_add_local_inputs_packed", _I32, [_P, _P, _I32]),
     ("rb_advance_frame", _I32, [_P]),
@@ -123,6 +124,7 @@ SIGNATURES = [
     ("rb_p2p_destroy", None, [_P]),
     ("rb_p2p_last_error", ctypes.c_char_p, [_P]),
     ("rb_p2p_set_stream", _I32, [_P, _P]),
+    ("rb_p2p_get_stream", _P, [_P]),
     ("rb_p2p_run_ticks", _I32, [_P, _I32, _P, ctypes.c_int64, _P, _P, _I32]),
     ("rb_p2p_read_status", _I32, [_P, _P, _P, _P, _P]),
     ("rb_p2p_disconnect_player", _I32, [_P, _I32, _P]),

@@ -23,6 +23,7 @@
 
 #include <atomic>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -123,10 +124,16 @@ struct rb_batch {
   uint32_t prof_every = 8, prof_tick = 0;
   bool staged = false;  // this tick's inputs went through the host staging buffer
   std::string last_err;
+  // Set when the device state and the host plan can no longer agree (an early
+  // fused launch ran ticks whose host bookkeeping then failed): every later
+  // call fails with RB_PANIC, as the reference process would have stopped.
+  std::string poisoned;
+  bool pipe = true;  // fused steady ticks with two ticks in flight (RB_STEADY_PIPE=0 at create: one at a time)
 };
 
 namespace {
 thread_local std::string g_create_err;
+constexpr size_t kProfPool = 256;  // HIP event pairs created by rb_profile_enable
 
 rb_status fail(rb_batch* b, rb_status st, const std::string& msg) {
   if (b) b->last_err = msg; else g_create_err = msg;
@@ -309,6 +316,7 @@ rb_status rb_synctest_create(const rb_config* cfg, rb_batch** out) {
   b->W = cfg->max_prediction;
   b->P = cfg->num_players;
   b->block = cfg->block_size ? static_cast<int>(cfg->block_size) : 256;
+  if (const char* env = std::getenv("RB_STEADY_PIPE")) b->pipe = std::atoi(env) != 0;
   if (b->block % 64 != 0 || b->block > 256) return fail(nullptr, RB_INVALID_REQUEST, "block_size must be 64, 128, 192 or 256");
   b->plan_only = cfg->device < 0;
   b->device = cfg->device;
@@ -387,6 +395,8 @@ rb_status rb_set_stream(rb_batch* b, void* s) {
   return RB_OK;
 }
 
+void* rb_get_stream(const rb_batch* b) { return b->plan_only ? nullptr : static_cast<void*>(b->stream); }
+
 int32_t rb_current_frame(const rb_batch* b) { return b->plan->current; }
 int32_t rb_num_sessions(const rb_batch* b) { return b->S; }
 int32_t rb_state_bytes(const rb_batch* b) { return b->ops->image_bytes; }
@@ -435,6 +445,7 @@ rb_status rb_add_local_inputs_packed(rb_batch* b, const void* inputs, int32_t on
 }
 
 rb_status rb_advance_frame(rb_batch* b) {
+  if (!b->poisoned.empty()) return fail(b, RB_PANIC, b->poisoned);
   rb_status result = RB_OK;
   // Checked mode: sessions frozen by the previous tick fail this call
   // (sync_test_session.rs:91-98 returns MismatchedChecksum before any work).
@@ -523,6 +534,7 @@ rb_status launch_steady_run(rb_batch* b, const uint8_t* tick_inputs, int64_t str
   r.live_out_last = 0;
   r.seed = b->cfg.seed;
   r.debug = b->cfg.reserved[0];
+  r.pipe = b->pipe ? 1 : 0;
   const bool timed = b->prof;
   if (timed) {
     if (b->prof_used == b->prof_ev.size()) {
@@ -548,6 +560,7 @@ rb_status launch_steady_run(rb_batch* b, const uint8_t* tick_inputs, int64_t str
 rb_status rb_run_ticks(rb_batch* b, int32_t n_ticks, const void* inputs, int64_t tick_stride_bytes,
                        int32_t on_device, int32_t* ticks_done) {
   if (ticks_done) *ticks_done = 0;
+  if (!b->poisoned.empty()) return fail(b, RB_PANIC, b->poisoned);
   if (n_ticks <= 0) return RB_OK;
   const size_t player_bytes = static_cast<size_t>(b->S) * b->ops->input_bytes;
   if (b->plan_only) {  // host bookkeeping only
@@ -654,6 +667,9 @@ rb_status rb_run_ticks(rb_batch* b, int32_t n_ticks, const void* inputs, int64_t
   }
   if (result == RB_OK) result = flush(done);
   else flush(done);
+  if (early && done < n_ticks)  // the device already ran all n ticks: it is ahead of the plan for good
+    b->poisoned = "batch poisoned: a fused launch ran " + std::to_string(n_ticks) + " ticks but the host bookkeeping stopped after " +
+                  std::to_string(done) + " (" + b->last_err + ")";
   if (tmp) (void)hipFreeAsync(tmp, b->stream);
   if (ticks_done) *ticks_done = done;
   if (result == RB_OK && (b->cfg.flags & RB_FLAG_CHECKED)) {
@@ -856,6 +872,17 @@ rb_status rb_profile_enable(rb_batch* b, int32_t on) {
   b->prof = on != 0;
   b->prof_every = on > 1 ? static_cast<uint32_t>(on) : 8u;
   b->prof_tick = 0;
+  // Create the event pool now, outside any timed region: a first hipEventCreate
+  // inside one costs tens of microseconds of host time.
+  if (b->prof && !b->plan_only) {
+    HIP_TRY(b, hipSetDevice(b->device));
+    while (b->prof_ev.size() < kProfPool) {
+      hipEvent_t e0 = nullptr, e1 = nullptr;
+      HIP_TRY(b, hipEventCreate(&e0));
+      HIP_TRY(b, hipEventCreate(&e1));
+      b->prof_ev.push_back({e0, e1});
+    }
+  }
   return RB_OK;
 }
 

@@ -292,6 +292,88 @@ struct ExGame {
       p[4] = __float_as_uint(pr.rot[j][k + 1]);
     }
   }
+  // The fused steady ticks' fast form of advance_prepared: no branch at all.
+  // The speed clamp's arithmetic (speed_clamp) is evaluated on every lane and
+  // selected where |v| > 7; the operand ranges its short division sequence
+  // does not cover (a zero or tiny component, a huge or infinite magnitude)
+  // are not handled here but flagged in `special`, and the caller re-runs the
+  // whole tick through the general form when any lane of the wave flagged one
+  // (kernels.hpp steady_kernel).  On every lane without a flag each f32
+  // operation is the one speed_clamp performs, so the bits are the same.
+  static constexpr bool kHasFast = true;
+  template <int N>
+  __device__ static void advance_prepared_fast(uint32_t (&w)[NWL], const Prep<N>& pr, int k, uint32_t& special) {
+#pragma unroll
+    for (int j = 0; j < kPlayersPerLane; ++j) {
+      uint32_t* p = &w[5 * j];
+      const float old_x = __uint_as_float(p[0]), old_y = __uint_as_float(p[1]);
+      float vx = __uint_as_float(p[2]) * kFriction + pr.tx[j][k];
+      float vy = __uint_as_float(p[3]) * kFriction + pr.ty[j][k];
+      const float m2 = vx * vx + vy * vy;
+      const bool clamp = m2 > kMaxSpeed * kMaxSpeed;  // see speed_clamp
+      const float mag = sqrt_rn_above_one(clamp ? m2 : 64.0f);
+      const float nx = vx * kMaxSpeed, ny = vy * kMaxSpeed;
+      const float r = rcp_refined(mag);
+      const float qx = div_rn_unscaled(nx, mag, r), qy = div_rn_unscaled(ny, mag, r);
+      const bool ok = mag < 256.0f && __builtin_fabsf(nx) >= 0x1p-96f && __builtin_fabsf(ny) >= 0x1p-96f;
+      special |= (clamp && !ok) ? 1u : 0u;
+      vx = clamp ? qx : vx;
+      vy = clamp ? qy : vy;
+      float x = old_x + vx, y = old_y + vy;
+      x = fminf(fmaxf(x, 0.0f), kWidth);
+      y = fminf(fmaxf(y, 0.0f), kHeight);
+      p[0] = __float_as_uint(x);
+      p[1] = __float_as_uint(y);
+      p[2] = __float_as_uint(vx);
+      p[3] = __float_as_uint(vy);
+      p[4] = __float_as_uint(pr.rot[j][k + 1]);
+    }
+  }
+  // One AdvanceFrame without any branch, for callers that redo the frame in
+  // the general form (advance) when any lane of the wave flags `special`: a
+  // rotation outside [+0, 6.5) (in_range) or a clamp operand outside the short
+  // division sequence.  Unflagged lanes get advance's bits: the rotation step
+  // and sincos are the in-range forms (exact there, see in_range), the thrust
+  // and clamp the operations of advance_player / advance_prepared_fast.
+  __device__ static void advance_fast(uint32_t (&w)[NWL], InRec rec, int lane, uint32_t disconnected_mask,
+                                      uint32_t& special) {
+#pragma unroll
+    for (int j = 0; j < kPlayersPerLane; ++j) {
+      const int i = kSplit ? lane : j;
+      const uint32_t input = ((disconnected_mask >> i) & 1u) ? 4u : player_input(rec, i);  // Disconnected => 4 (:268)
+      uint32_t* p = &w[5 * j];
+      const float rot = __uint_as_float(p[4]);
+      special |= __float_as_uint(rot) < 0x40D00000u ? 0u : 1u;  // +0 <= rot < 6.5
+      const bool up = input & 1u, down = input & 2u, left = input & 4u, right = input & 8u;
+      const SinCos sc = sincosf_glibc<true>(rot, nullptr);
+      const float sp = up ? kMovementSpeed : -kMovementSpeed;
+      const float tx = sp * sc.c, ty = sp * sc.s;  // -(S * c) == (-S) * c
+      const uint32_t thm = up != down ? ~0u : 0u;
+      const float txm = __uint_as_float((thm & __float_as_uint(tx)) | (~thm & 0x80000000u));
+      const float tym = __uint_as_float((thm & __float_as_uint(ty)) | (~thm & 0x80000000u));
+      const float r1 = rem_euclid_near<true>(rot + (left ? -kRotationSpeed : kRotationSpeed), 2.0f * kPi);
+      float vx = __uint_as_float(p[2]) * kFriction + txm;
+      float vy = __uint_as_float(p[3]) * kFriction + tym;
+      const float m2 = vx * vx + vy * vy;
+      const bool clamp = m2 > kMaxSpeed * kMaxSpeed;
+      const float mag = sqrt_rn_above_one(clamp ? m2 : 64.0f);
+      const float nx = vx * kMaxSpeed, ny = vy * kMaxSpeed;
+      const float r = rcp_refined(mag);
+      const float qx = div_rn_unscaled(nx, mag, r), qy = div_rn_unscaled(ny, mag, r);
+      const bool ok = mag < 256.0f && __builtin_fabsf(nx) >= 0x1p-96f && __builtin_fabsf(ny) >= 0x1p-96f;
+      special |= (clamp && !ok) ? 1u : 0u;
+      vx = clamp ? qx : vx;
+      vy = clamp ? qy : vy;
+      float x = __uint_as_float(p[0]) + vx, y = __uint_as_float(p[1]) + vy;
+      x = fminf(fmaxf(x, 0.0f), kWidth);
+      y = fminf(fmaxf(y, 0.0f), kHeight);
+      p[0] = __float_as_uint(x);
+      p[1] = __float_as_uint(y);
+      p[2] = __float_as_uint(vx);
+      p[3] = __float_as_uint(vy);
+      p[4] = left != right ? __float_as_uint(r1) : __float_as_uint(rot);
+    }
+  }
   // A rotation in [+0, 6.5) steps to rot +- 2.5/60 in (-2pi, 4pi), which
   // rem_euclid maps into [+0, 2pi] with one add or subtract (rem_euclid_near;
   // never -0); from there every later step stays in that interval.  So a state

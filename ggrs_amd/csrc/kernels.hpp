@@ -149,6 +149,45 @@ __device__ __forceinline__ unsigned step_slot(const KParams& p, int k) {
   return static_cast<unsigned>(sl);
 }
 
+// G::kHasFast (games.hpp ExGame::advance_prepared_fast), false when not declared
+template <class G, class = void>
+struct HasFast {
+  static constexpr bool value = false;
+};
+template <class G>
+struct HasFast<G, std::void_t<decltype(G::kHasFast)>> {
+  static constexpr bool value = G::kHasFast;
+};
+template <class G, class Pr>
+__device__ __forceinline__ void advance_fast(uint32_t (&w)[G::NWL], const Pr& pr, int k, uint32_t& special) {
+  if constexpr (HasFast<G>::value) G::advance_prepared_fast(w, pr, k, special);
+}
+#ifndef RB_FAST_ADVANCE
+#define RB_FAST_ADVANCE 1  // 0: the branchy AdvanceFrame everywhere (A/B builds, tools/mkvar.sh)
+#endif
+// One AdvanceFrame{inputs} (State::advance, ex_game.rs:259-321) for the
+// kernels that run frames one at a time (tick_kernel, p2p_kernel, the
+// fan-out): a game with G::kHasFast runs its branch-free form, and the wave
+// redoes the frame in the general form from the same state when any active
+// lane flagged an operand the fast form does not cover.
+template <class G>
+__device__ __forceinline__ void advance_frame(uint32_t (&w)[G::NWL], typename G::InRec in, int lane, uint32_t dmask,
+                                              uint32_t* unexpected) {
+  if constexpr (HasFast<G>::value && RB_FAST_ADVANCE) {
+    uint32_t w0[G::NWL];
+#pragma unroll
+    for (int i = 0; i < G::NWL; ++i) w0[i] = w[i];
+    uint32_t special = 0;
+    G::advance_fast(w, in, lane, dmask, special);
+    if (__any(special != 0u)) {
+#pragma unroll
+      for (int i = 0; i < G::NWL; ++i) w[i] = w0[i];
+      G::advance(w, in, lane, dmask, unexpected);
+    }
+  } else {
+    G::advance(w, in, lane, dmask, unexpected);
+  }
+}
 // The fused tick.  Thread g serves lane (g % L) of session g / L; a session's
 // state slice stays in that lane's VGPRs for the whole tick.  Phase 1 issues
 // every load of the tick (frozen mask, new inputs, the loaded snapshot, the
@@ -251,7 +290,7 @@ __global__ void __launch_bounds__(256) tick_kernel(const KParams p) {
       if (p.debug & 1u)
         w[0] += in[k];
       else
-        G::advance(w, in[k], lane, p.disc_mask, &p.counters[1]);  // AdvanceFrame{inputs}
+        advance_frame<G>(w, in[k], lane, p.disc_mask, &p.counters[1]);  // AdvanceFrame{inputs}
       if (step == p.periodic_step) {
         ctx.nonce = p.nonce_base + 128u + static_cast<uint32_t>(step);
         const CS c = G::checksum(w, f + 1, lane, ctx);
@@ -314,6 +353,7 @@ struct RunParams {
   int32_t live_out_last;    // store the live state after the last tick
   uint64_t seed;
   uint32_t debug;           // experiment knobs (rb_config.reserved[0]); 0 in every real run
+  int32_t pipe;             // 1: two ticks in flight per lane where the game allows it (steady_pipe.hpp)
 };
 
 // An empty asm that reads v: the compiler must complete the load that
@@ -351,6 +391,9 @@ struct DecSel<G, true> {
 };
 template <class G>
 using DecOf = typename DecSel<G>::type;
+#ifndef RB_STEADY_FAST
+#define RB_STEADY_FAST 1  // 0: the branchy form on every tick (A/B builds, tools/mkvar.sh)
+#endif
 
 // kExp: attribution experiments (RunParams::debug knobs, tools/exp_steady.py);
 // instantiated only in builds made with RB_EXPERIMENTS=1, never in the product.
@@ -474,8 +517,13 @@ __global__ void __launch_bounds__(256) steady_kernel(const RunParams p) {
     // (group_sum), so the checksum stores are issued by every lane: the lanes
     // of a session write the same value to the same address, and no exec-mask
     // branch splits the tick into separately scheduled blocks.
-    auto steps = [&](auto in_range_tag) __attribute__((always_inline)) {
+    // kFast (in-range ticks of a game with G::kHasFast): the branch-free AdvanceFrame, whose
+    // flagged lanes (operands outside its short division sequence) make the wave redo the tick
+    // in the general form below; returns this lane's flag.
+    auto steps = [&](auto in_range_tag, auto fast_tag) __attribute__((always_inline)) -> uint32_t {
     constexpr bool kInRange = decltype(in_range_tag)::value;
+    constexpr bool kFast = decltype(fast_tag)::value;
+    uint32_t special = 0;
     [[maybe_unused]] PrepOf<G, CD + 1> prep;
     if constexpr (G::kHasPrep && !kExp)  // the tick's rotation chain and thrust first (games.hpp)
       G::template prepare<kInRange, CD + 1>(w, dec, prep, &p.counters[1]);
@@ -503,17 +551,39 @@ __global__ void __launch_bounds__(256) steady_kernel(const RunParams p) {
       }
       if (dbg & 1u)
         w[0] += win[k];
+      else if constexpr (kFast && !kExp)
+        advance_fast<G>(w, prep, k, special);  // AdvanceFrame{inputs}
       else if constexpr (G::kHasPrep && !kExp)
         G::advance_prepared(w, prep, k);  // AdvanceFrame{inputs}
       else
         G::template advance<kInRange>(w, (dbg & 32u) ? static_cast<InRec>(win[k] & static_cast<InRec>(dbg >> 8)) : win[k],
                                       lane, 0u, &p.counters[1]);  // AdvanceFrame{inputs}
     }
+    return special;
     };
-    if (G::kHasRangePath && __all(G::in_range(w)))
-      steps(std::true_type{});
-    else
-      steps(std::false_type{});
+    if (G::kHasRangePath && __all(G::in_range(w))) {
+      if constexpr (HasFast<G>::value && RB_STEADY_FAST && !kExp) {
+        // Optimistic: every lane of the wave runs the branch-free tick; if any lane met an
+        // operand its division sequence does not cover, the wave runs the tick again from the
+        // loaded state in the general form.  The redo re-executes every request of the tick:
+        // it stores the same cells, checksums and first-seen record over the first pass's (same
+        // lanes, same addresses, program order), re-decides the mismatch and reloads the next
+        // tick's cell.
+        uint32_t w0[NW];
+#pragma unroll
+        for (int i = 0; i < NW; ++i) w0[i] = w[i];
+        if (__any(steps(std::true_type{}, std::true_type{}) != 0u)) {
+#pragma unroll
+          for (int i = 0; i < NW; ++i) w[i] = w0[i];
+          mismatch = kNullFrame;
+          steps(std::false_type{}, std::false_type{});
+        }
+      } else {
+        steps(std::true_type{}, std::false_type{});
+      }
+    } else {
+      steps(std::false_type{}, std::false_type{});
+    }
     if constexpr (G::kDisplay) {
       // Game::last_checksum after the final AdvanceFrame (frame c+1) and the periodic checksum
       // when c+1 is a multiple of 100, as the session leaves the launch: at its last tick, or at
@@ -566,6 +636,10 @@ __global__ void __launch_bounds__(256) steady_kernel(const RunParams p) {
     slot0 = slot_after(slot0, 1);
   }
 }
+
+}  // namespace rb
+#include "steady_pipe.hpp"  // two ticks in flight per lane (uses settle / HasFast above)
+namespace rb {
 
 template <class G>
 __global__ void report_kernel(const typename G::CS* __restrict__ cs, const int32_t* __restrict__ err, int S,
@@ -644,6 +718,12 @@ struct GameOpsT final : GameOps {
 #else
       return hipErrorNotSupported;  // experiment knobs need a RB_EXPERIMENTS=1 build
 #endif
+    }
+    if constexpr (G::kHasPrep && HasFast<G>::value && CD >= 3 && CD % 2 == 1) {
+      if (p.pipe) {
+        hipLaunchKernelGGL((steady_pipe_kernel<G, CD>), dim3(grid), dim3(block), 0, st, p);
+        return hipGetLastError();
+      }
     }
     hipLaunchKernelGGL((steady_kernel<G, CD, false>), dim3(grid), dim3(block), 0, st, p);
     return hipGetLastError();

@@ -644,7 +644,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     ++nadv;
     if (exec) {
       if constexpr (RB_P2P_EXP & 1) w[0] += static_cast<uint32_t>(in);  // attribution builds only
-      else G::advance(w, in, lane, dmask, &p.counters[1]);
+      else advance_frame<G>(w, in, lane, dmask, &p.counters[1]);
       ++tot_adv;
     }
   };
@@ -733,18 +733,23 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     const unsigned col = !indep ? (s * kSpecBranches + static_cast<unsigned>(kk)) * L + lane
                                 : s * kIndepLanes + (lane == rs ? static_cast<unsigned>(kk) : kSpecBranches + lane);
     const CS* __restrict__ scs = reinterpret_cast<const CS*>(p.spec_cs);
+    // the padding lane of a 4-lane group (P = 3) holds no player: no branch column was written
+    // for it (fanout_indep_kernel), so it keeps its own words; nothing observes them
+    const bool real = !kSplit || lane < P;
     for (int32_t f = base + 1; f < cur; ++f) {  // the cells adjust would have saved
       const unsigned slot = static_cast<unsigned>(f % W);
-      uint32_t cw[NW];
-      load_words<NW>(p.spec_cells + slot * NW * Gs, static_cast<int>(Gs), static_cast<int>(col), cw);
-      store_words<NW>(p.snap + slot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), cw);
+      if (real) {
+        uint32_t cw[NW];
+        load_words<NW>(p.spec_cells + slot * NW * Gs, static_cast<int>(Gs), static_cast<int>(col), cw);
+        store_words<NW>(p.snap + slot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), cw);
+      }
       if (lead) {
         csa[slot * Spad + s] = scs[(slot * Spad + s) * kSpecBranches + kk];
         p.tag[slot * Spad + s] = f;
       }
       ++tot_save;
     }
-    load_words<NW>(p.spec_state, static_cast<int>(Gs), static_cast<int>(col), w);
+    if (real) load_words<NW>(p.spec_state, static_cast<int>(Gs), static_cast<int>(col), w);
     ++tot_sel;
     return true;
   };
@@ -1274,8 +1279,8 @@ __global__ void __launch_bounds__(256) fanout_kernel(const FanParams p) {
       else if (local || (la_h != kNullFrame && f <= la_h)) v = ring.get(f, h, s);  // Confirmed
       else v = pred;  // repeat-last prediction (blank before the first input)
     }
-    G::advance(w, static_cast<InRec>(static_cast<uint64_t>(v) << (8 * IB * (active ? h : 0))), lane, 0u,
-               &p.counters[1]);
+    advance_frame<G>(w, static_cast<InRec>(static_cast<uint64_t>(v) << (8 * IB * (active ? h : 0))), lane, 0u,
+                     &p.counters[1]);
     ++frames;
   }
   store_words<NW>(p.spec_state, static_cast<int>(Gs), static_cast<int>(g), w);
@@ -1376,7 +1381,7 @@ __global__ void __launch_bounds__(256) fanout_indep_kernel(const FanParams p) {
     if (branch) v = static_cast<uint32_t>(k);
     else if (local || (la_h != kNullFrame && f <= la_h)) v = ring.get(f, h, s);  // Confirmed
     else v = pred;  // repeat-last prediction (blank before the first input)
-    G::advance(w, static_cast<InRec>(static_cast<uint64_t>(v) << (8 * IB * h)), h, 0u, &p.counters[1]);
+    advance_frame<G>(w, static_cast<InRec>(static_cast<uint64_t>(v) << (8 * IB * h)), h, 0u, &p.counters[1]);
     ++frames;
   }
   store_words<NW>(p.spec_state, static_cast<int>(Gs), static_cast<int>(col), w);

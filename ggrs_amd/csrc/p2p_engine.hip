@@ -353,6 +353,8 @@ rb_status rb_p2p_set_stream(rb_p2p* b, void* s) {
   return RB_OK;
 }
 
+void* rb_p2p_get_stream(const rb_p2p* b) { return static_cast<void*>(b->stream); }
+
 int32_t rb_p2p_state_bytes(const rb_p2p* b) { return b->ops->image_bytes; }
 int32_t rb_p2p_input_bytes(const rb_p2p* b) { return b->ops->input_bytes; }
 
@@ -656,6 +658,16 @@ rb_status rb_p2p_debug_corrupt(rb_p2p* b, int32_t session, int32_t word, uint32_
 
 rb_status rb_p2p_profile_enable(rb_p2p* b, int32_t on) {
   b->prof = on != 0;
+  // the event pool is created here, outside any timed region
+  if (b->prof) {
+    P2P_TRY(b, hipSetDevice(b->device));
+    while (b->prof_ev.size() < 256) {
+      hipEvent_t e0 = nullptr, e1 = nullptr;
+      P2P_TRY(b, hipEventCreate(&e0));
+      P2P_TRY(b, hipEventCreate(&e1));
+      b->prof_ev.emplace_back(e0, e1);
+    }
+  }
   return RB_OK;
 }
 

@@ -17,7 +17,7 @@ import enum
 import numpy as np
 
 from . import _lib as L
-from .session import DeviceError, InvalidRequest, Panic, input_dtype
+from .session import DeviceError, InvalidRequest, Panic, _StreamOrdered, input_dtype
 from .synth import SEED, splitmix64
 
 
@@ -35,8 +35,14 @@ def _dev_ptr(x):
     return ctypes.c_void_p(x.data_ptr()), x
 
 
-class P2PSession:
-    """p2p_session.rs:116-929 (rollback path) for ``num_sessions`` sessions."""
+class P2PSession(_StreamOrdered):
+    """p2p_session.rs:116-929 (rollback path) for ``num_sessions`` sessions.
+
+    Device work runs on the batch's own HIP stream (or the one set_stream
+    chose) and is ordered against torch's current stream at every call
+    (_StreamOrdered): inputs made on torch's stream are complete before a
+    launch reads them, and tensors a call writes (checksum reports) are
+    complete before later torch work on the current stream reads them."""
 
     def __init__(self, lib, handle, game, cfg):
         self._lib = lib
@@ -52,12 +58,15 @@ class P2PSession:
         self.desync_interval = int(cfg.desync_interval)
         self.state_bytes = lib.rb_p2p_state_bytes(handle)
         self.input_dtype = input_dtype(game, lib.rb_p2p_input_bytes(handle))
-        self._keep = []
+        self._device = int(cfg.device)
+        self._bind(self._device, lib.rb_p2p_get_stream(handle) or 0)
 
     def close(self):
         if self._h:
-            self._lib.rb_p2p_destroy(self._h)
+            self._lib.rb_p2p_destroy(self._h)  # synchronises the batch stream first
             self._h = None
+            self._stream = None
+            self._drain()
 
     def __del__(self):
         try:
@@ -78,6 +87,7 @@ class P2PSession:
 
     def set_stream(self, stream) -> None:
         self._check(self._lib.rb_p2p_set_stream(self._h, ctypes.c_void_p(stream.cuda_stream if stream else 0)))
+        self._bind(self._device, self._lib.rb_p2p_get_stream(self._h) or 0)
 
     def run_ticks(self, local_inputs, remote_upto, remote_inputs) -> None:
         """T ticks: [poll_remote_clients, add_local_input for every local handle,
@@ -94,9 +104,10 @@ class P2PSession:
         lp, lk = _dev_ptr(local_inputs)
         up, uk = _dev_ptr(remote_upto)
         rp, rk = _dev_ptr(remote_inputs)
-        self._keep = [lk, uk, rk]
+        cur = self._pre()
         stride = self.num_players * self.num_sessions * lk.element_size()
         self._check(self._lib.rb_p2p_run_ticks(self._h, T, lp, stride, up, rp, int(remote_inputs.shape[0])))
+        self._post(cur, (lk, uk, rk))
 
     def disconnect_player(self, handle: int, sessions=None) -> None:
         """P2PSession::disconnect_player(handle) (p2p_session.rs:430-456) in every
@@ -173,14 +184,17 @@ class P2PSession:
         """The ChecksumReports every session sent since the last call, oldest
         first, as a CUDA int64 tensor [RB_P2P_REPORTS_PER_TAKE, S, 3] (one
         rb_checksum_report per row: checksum lo, hi, frame | mismatch << 32;
-        frame NULL_FRAME = none).  Stream-ordered; `out` may be reused."""
+        frame NULL_FRAME = none).  Ordered against torch's current stream
+        (_StreamOrdered): later work on it sees the reports; `out` may be reused."""
         import torch
         from .shard import REPORT_WORDS
         K = L.RB_P2P_REPORTS_PER_TAKE
         if out is None:
             out = torch.empty((K, self.num_sessions, REPORT_WORDS), dtype=torch.int64, device="cuda")
         assert out.is_cuda and out.is_contiguous() and tuple(out.shape) == (K, self.num_sessions, REPORT_WORDS)
+        cur = self._pre()
         self._check(self._lib.rb_p2p_take_checksum_reports(self._h, ctypes.c_void_p(out.data_ptr())))
+        self._post(cur, (out,), outputs=True)
         return out
 
     def receive_checksum_reports(self, handle: int, reports) -> None:
@@ -188,8 +202,9 @@ class P2PSession:
         tensor, take_checksum_reports layout): UdpProtocol::on_checksum_report."""
         r, keep = _dev_ptr(reports)
         assert keep.dim() == 3 and keep.shape[1] == self.num_sessions
-        self._keep = [keep]
+        cur = self._pre()
         st = self._lib.rb_p2p_receive_checksum_reports(self._h, int(handle), r, int(keep.shape[0]))
+        self._post(cur, (keep,))
         if st == L.RB_INVALID_REQUEST:
             raise InvalidRequest((self._lib.rb_p2p_last_error(self._h) or b"").decode())
         self._check(st)
@@ -214,8 +229,9 @@ class P2PSession:
         lp, lk = _dev_ptr(last_frames)
         dp, dk = _dev_ptr(disconnected)
         assert tuple(lk.shape) == (self.num_players, self.num_sessions) and tuple(dk.shape) == tuple(lk.shape)
-        self._keep = [lk, dk]
+        cur = self._pre()
         st = self._lib.rb_p2p_receive_peer_connect_status(self._h, int(endpoint), lp, dp)
+        self._post(cur, (lk, dk))
         if st == L.RB_INVALID_REQUEST:
             raise InvalidRequest((self._lib.rb_p2p_last_error(self._h) or b"").decode())
         self._check(st)

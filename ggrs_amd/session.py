@@ -314,8 +314,73 @@ class SessionBuilder:
         return SyncTestSession(lib, h, game_of(self._cfg.game), self._cfg)
 
 
+# --------------------------------------------------------------------------- stream ordering
+class _StreamOrdered:
+    """Orders a batch's device work against torch's current stream.
+
+    A device batch runs on its own HIP stream unless ``set_stream`` chose
+    another (rb_get_stream says which).  When torch's current stream is not
+    that stream at a call, the call (1) makes the batch stream wait for the
+    work queued on torch's stream so far (device inputs made there are
+    complete before a launch reads them), (2) keeps the tensors it handed to
+    the device referenced until an event recorded after its launches has
+    completed (the caching allocator cannot hand their memory to torch's
+    stream while a launch may still read it), and (3) for calls that write a
+    caller tensor, makes torch's stream wait for the batch stream.  When the
+    streams are the same, stream order already gives all three and nothing is
+    added."""
+
+    _stream = None  # the batch's HIP stream as a torch stream object, or None (plan-only)
+    _inflight = None  # deque of (event, tensors) of calls still possibly reading their tensors
+
+    def _bind(self, device: int, handle: int):
+        """Wrap the batch's stream (rb_get_stream / rb_p2p_get_stream) for torch."""
+        self._stream = None
+        if device < 0 or not handle:
+            return
+        import torch
+        if torch.cuda.is_available():
+            self._stream = torch.cuda.ExternalStream(int(handle), device=torch.device("cuda", device))
+
+    def _pre(self):
+        """Before a launching call: the torch stream to order against, or None (same stream)."""
+        st = self._stream
+        if st is None:
+            return None
+        import torch
+        cur = torch.cuda.current_stream(st.device)
+        if cur.cuda_stream == st.cuda_stream:
+            return None
+        st.wait_stream(cur)
+        return cur
+
+    def _post(self, cur, tensors=(), outputs=False):
+        """After a launching call that _pre ordered against `cur`."""
+        if cur is None:
+            return
+        import collections
+
+        import torch
+        st = self._stream
+        if tensors:
+            if self._inflight is None:
+                self._inflight = collections.deque()
+            ev = torch.cuda.Event()
+            ev.record(st)
+            self._inflight.append((ev, tensors))
+        while self._inflight and self._inflight[0][0].query():
+            self._inflight.popleft()
+        if outputs:
+            cur.wait_stream(st)
+
+    def _drain(self):
+        """After the batch stream was synchronised (close): nothing is in flight."""
+        if self._inflight:
+            self._inflight.clear()
+
+
 # --------------------------------------------------------------------------- session
-class SyncTestSession:
+class SyncTestSession(_StreamOrdered):
     """sync_test_session.rs:11-204 for ``num_sessions`` sessions at once."""
 
     def __init__(self, lib, handle, game: Game, cfg):
@@ -331,12 +396,16 @@ class SyncTestSession:
         self.state_bytes = lib.rb_state_bytes(handle)
         self.input_dtype = input_dtype(game, lib.rb_input_bytes(handle))
         self._keep = []  # host arrays referenced by queued copies
+        self._device = int(cfg.device)
+        self._bind(self._device, lib.rb_get_stream(handle) or 0)
 
     # -- lifetime
     def close(self):
         if self._h:
-            self._lib.rb_destroy(self._h)
+            self._lib.rb_destroy(self._h)  # synchronises the batch stream first
             self._h = None
+            self._stream = None
+            self._drain()
 
     def __del__(self):
         try:
@@ -379,19 +448,25 @@ class SyncTestSession:
         CUDA tensor (stays on the device)."""
         ptr, dev, keep = self._as_input(inputs, self.num_sessions)
         self._keep.append(keep)
+        cur = self._pre() if dev else None
         _raise(self._lib, self._h, self._lib.rb_add_local_input(self._h, int(player_handle), ptr, dev))
+        self._post(cur)  # the tensor stays in _keep until advance_frame has launched
 
     def add_local_inputs(self, inputs) -> None:
         """All handles at once: [num_sessions, num_players] values."""
         ptr, dev, keep = self._as_input(inputs, self.num_sessions * self._num_players)
         self._keep.append(keep)
+        cur = self._pre() if dev else None
         _raise(self._lib, self._h, self._lib.rb_add_local_inputs_packed(self._h, ptr, dev))
+        self._post(cur)
 
     def advance_frame(self) -> "RequestList":  # :85-146
         """Runs SyncTestSession::advance_frame and the game's handle_requests
         for every session; returns the request stream that was executed
         (a list of GGRSRequest, decoded lazily)."""
+        cur = self._pre()
         st = self._lib.rb_advance_frame(self._h)
+        self._post(cur, tuple(k for k in self._keep if hasattr(k, "data_ptr")))
         self._keep.clear()
         if st == L.RB_MISMATCHED_CHECKSUM:
             raise MismatchedChecksum(self.mismatches())
@@ -405,9 +480,11 @@ class SyncTestSession:
         T = int(inputs.shape[0])
         per_tick = self._num_players * self.num_sessions
         ptr, dev, keep = self._as_input(inputs, T * per_tick) if T else (None, 0, None)
+        cur = self._pre() if dev else None
         done = ctypes.c_int32()
         st = self._lib.rb_run_ticks(self._h, T, ptr, per_tick * np.dtype(self.input_dtype).itemsize, dev,
                                     ctypes.byref(done))
+        self._post(cur, (keep,))
         if st == L.RB_MISMATCHED_CHECKSUM:
             raise MismatchedChecksum(self.mismatches())
         _raise(self._lib, self._h, st)
@@ -435,6 +512,7 @@ class SyncTestSession:
         """Run on a caller stream (int handle or torch.cuda.Stream)."""
         ptr = getattr(stream, "cuda_stream", stream)
         _raise(self._lib, self._h, self._lib.rb_set_stream(self._h, ctypes.c_void_p(ptr)))
+        self._bind(self._device, self._lib.rb_get_stream(self._h) or 0)
 
     def read_cell(self, frame: int):
         """(images [S, state_bytes] u8, checksums [S, 2] u64 lo/hi) of the cell holding ``frame``."""
@@ -456,8 +534,13 @@ class SyncTestSession:
         return img, dcs, fr
 
     def export_checksum_report(self, frame: int, dev_ptr: int) -> None:
-        """Write [S] rb_checksum_report (32 B each) for ``frame`` to device memory."""
-        _raise(self._lib, self._h, self._lib.rb_export_checksum_report(self._h, int(frame), ctypes.c_void_p(dev_ptr)))
+        """Write [S] rb_checksum_report (24 B each) for ``frame`` to device memory
+        (a pointer, or a CUDA tensor); torch's current stream waits for it."""
+        is_t = hasattr(dev_ptr, "data_ptr")
+        ptr = dev_ptr.data_ptr() if is_t else dev_ptr
+        cur = self._pre()
+        _raise(self._lib, self._h, self._lib.rb_export_checksum_report(self._h, int(frame), ctypes.c_void_p(ptr)))
+        self._post(cur, (dev_ptr,) if is_t else (), outputs=True)
 
     def debug_corrupt_cell(self, session: int, frame: int, word: int, xor_mask: int) -> None:
         _raise(self._lib, self._h, self._lib.rb_debug_corrupt_cell(

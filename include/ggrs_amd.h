@@ -111,6 +111,10 @@ const char* rb_last_error(const rb_batch* b);
 /* Run this batch on a caller-owned hipStream_t (passed as void*); NULL = the
  * batch's own stream. */
 rb_status rb_set_stream(rb_batch* b, void* hip_stream);
+/* The hipStream_t the batch runs on (its own one unless rb_set_stream chose
+ * another); NULL for a plan-only batch.  Callers order their own streams
+ * against it (ggrs_amd/session.py _StreamOrdered). */
+void* rb_get_stream(const rb_batch* b);
 
 /* SyncTestSession::add_local_input (sync_test_session.rs:61-74) for every
  * session at once: `inputs` holds S values of the game's Input type
@@ -218,7 +222,8 @@ rb_status rb_profile_take(rb_batch* b, double* total_ms, int32_t* launches);
  * (`remote_upto`) and the inputs by frame (`remote_inputs`).  Mispredicted
  * remote inputs roll sessions back individually (per-session depth), on the
  * device.  rb_p2p_disconnect_player covers disconnects the user issues;
- * spectators, time sync and peer-reported disconnects are out of scope.
+ * peer-reported disconnects arrive through rb_p2p_receive_peer_connect_status
+ * (RB_P2P_FLAG_PEER_STATUS, below).  Spectators and time sync are out of scope.
  * ======================================================================== */
 typedef struct rb_p2p rb_p2p;
 
@@ -233,7 +238,7 @@ typedef struct rb_p2p_config {
   uint32_t local_mask;    /* bit h: handle h is PlayerType::Local; at least one local and one remote */
   int32_t remote_delay;   /* frame of each remote handle's first Event::Input (the peer's input delay) */
   int32_t sparse_saving;  /* with_sparse_saving_mode (builder.rs:159-166) */
-  uint32_t flags;         /* RB_FLAG_LANE_PER_SESSION, RB_P2P_FLAG_FANOUT */
+  uint32_t flags;         /* RB_FLAG_LANE_PER_SESSION, RB_P2P_FLAG_FANOUT, RB_P2P_FLAG_PEER_STATUS */
   uint32_t block_size;
   int32_t desync_interval; /* with_desync_detection_mode (builder.rs:167-172): DesyncDetection::On{interval}
                               for interval > 0, Off for 0 (the default, builder.rs:15) */
@@ -265,6 +270,7 @@ rb_status rb_p2p_create(const rb_p2p_config* cfg, rb_p2p** out);
 void rb_p2p_destroy(rb_p2p* b);
 const char* rb_p2p_last_error(const rb_p2p* b);
 rb_status rb_p2p_set_stream(rb_p2p* b, void* hip_stream);
+void* rb_p2p_get_stream(const rb_p2p* b);  /* as rb_get_stream */
 
 /* n_ticks x [poll_remote_clients + add_local_input for every local handle +
  * advance_frame (p2p_session.rs:253-337) + handle_requests] for every session,

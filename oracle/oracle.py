@@ -57,6 +57,8 @@ def load(path: str = LIB_PATH):
             "orc_synth_inputs": (None, [U64, ctypes.c_uint32, I32, I32, I32, I32, I32, P]),
             "orc_bench_exgame": (ctypes.c_double, [I32, I32, I32, I32, I32, I32, I32, I32, U64, PI32]),
             "orc_bench_brawler": (ctypes.c_double, [I32, I32, I32, I32, I32, I32, I32, I32, U64, PI32]),
+            "orc_bench_exgame_soa": (ctypes.c_double, [I32, I32, I32, I32, I32, I32, I32, I32, U64, PI32]),
+            "orc_soa_exgame_run": (I32, [I32, I32, I32, I32, I32, I32, I32, P, P, P]),
             "orc_p2p_create": (P, [I32, I32, I32, I32, ctypes.c_uint32, I32, I32, I32]),
             "orc_p2p_destroy": (None, [P]),
             "orc_p2p_last_panic": (ctypes.c_char_p, [P]),
@@ -324,6 +326,29 @@ def bench_exgame(num_players: int, check_distance: int, input_delay: int, max_pr
     t = load().orc_bench_exgame(num_players, check_distance, input_delay, max_prediction, sessions, warmup, ticks,
                                 threads, seed, ctypes.byref(ne))
     return t, ne.value
+
+
+def bench_exgame_soa(num_players: int, check_distance: int, input_delay: int, max_prediction: int, sessions: int,
+                     warmup: int, ticks: int, threads: int, seed: int):
+    """CPU 'optimized' baseline (oracle/soa_baseline.cpp: no per-request allocation,
+    closed-form fletcher16, cache-blocked sessions): wall seconds of `ticks` ticks."""
+    ne = ctypes.c_int32()
+    t = load().orc_bench_exgame_soa(num_players, check_distance, input_delay, max_prediction, sessions, warmup, ticks,
+                                    threads, seed, ctypes.byref(ne))
+    return t, ne.value
+
+
+def soa_exgame_run(num_players: int, check_distance: int, input_delay: int, max_prediction: int, inputs,
+                   threads: int = 2):
+    """The optimized baseline's results after len(inputs) ticks from frame 0 (TEST ONLY):
+    (live states [S, P, 5] f32 as x, y, vx, vy, rot; Game::last_checksum [S] u16; errors)."""
+    T, P, S = inputs.shape
+    a = np.ascontiguousarray(inputs, np.uint8)
+    st = np.zeros((S, P, 5), np.float32)
+    cs = np.zeros(S, np.uint16)
+    ne = load().orc_soa_exgame_run(P, check_distance, input_delay, max_prediction, S, T, threads, _ptr(a), _ptr(st),
+                                   _ptr(cs))
+    return st, cs, ne
 
 
 def bench_brawler(num_players: int, check_distance: int, input_delay: int, max_prediction: int, sessions: int,

@@ -317,6 +317,46 @@ def test_bench_config_65536_sessions_sampled_parity(gpu_available):
         np.testing.assert_array_equal(gc[sample], ocs[w])
 
 
+def test_bench_config_65536_sessions_fused_path_sampled_parity(gpu_available):
+    """BASELINE config 2 at exactly 65,536 sessions through the path bench.py
+    times (rb_run_ticks: the fused steady_kernel), in the driver's chunks: 8
+    start-up ticks, a 5-tick warmup launch, a 20-tick launch (the timed one),
+    then a 50-tick launch and 7 one-tick calls (the realtime block).  No
+    session mismatches; 64 sampled sessions are bit-exact with the oracle
+    (live state, display checksums, every cell)."""
+    import torch
+    S, P = 65536, 2
+    chunks = [8, 5, 20, 50] + [1] * 7
+    T = sum(chunks)
+    inputs = synth_inputs(S, P, T)
+    sess = (G.SessionBuilder(G.Game.EX_GAME, num_sessions=S).with_num_players(P).with_check_distance(7)
+            .with_input_delay(2).with_checked_mismatches(False).start_synctest_session())
+    dev = torch.from_numpy(inputs).cuda()
+    t = 0
+    for n in chunks:
+        assert sess.run_ticks(dev[t:t + n]) == n
+        t += n
+    assert sess.current_frame() == T
+    assert (sess.mismatches() == -1).all()
+    rng = np.random.default_rng(3)
+    sample = np.sort(rng.choice(S, 64, replace=False))
+    orc = O.OracleBatch(O.EX_GAME, P, 8, 7, 2, sample.size)
+    for t in range(T):
+        for h in range(P):
+            orc.add_local_input(h, inputs[t, h, sample])
+        k, _ = orc.advance()
+        assert (k == 0).all()
+    gimg, gdcs, _ = sess.read_live()
+    oimg, odcs, _ = orc.read_live()
+    np.testing.assert_array_equal(gimg[sample], oimg)
+    np.testing.assert_array_equal(gdcs[sample], odcs)
+    frames, oc, _, ocs = orc.read_cells()
+    for w, fr in enumerate(frames):
+        gi, gc = sess.read_cell(int(fr))
+        np.testing.assert_array_equal(gi[sample], oc[w])
+        np.testing.assert_array_equal(gc[sample], ocs[w])
+
+
 def test_config5_shard_131072_sessions_with_audit_replicas(gpu_available):
     """BASELINE config 5's per-GPU shard as bench.py --gpus 8 runs it on rank 7:
     global sessions [7*131072, 8*131072) plus 64 audit replicas of rank 0's
@@ -377,12 +417,15 @@ def test_config5_shard_131072_sessions_with_audit_replicas(gpu_available):
                                            (G.Game.EX_GAME, 1, 8, 4, 0), (G.Game.EX_GAME, 3, 6, 5, 1),
                                            (G.Game.EX_GAME, 4, 9, 8, 3), (G.Game.EX_GAME, 2, 12, 11, 2),
                                            (G.Game.STUB, 2, 8, 7, 2), (G.Game.STUB, 2, 8, 2, 0),
-                                           (G.Game.STUB_ENUM, 2, 8, 3, 1)])
-def test_run_ticks_fused_parity(gpu_available, game, P, W, cd, d):
+                                           (G.Game.STUB_ENUM, 2, 8, 3, 1), (G.Game.EX_GAME, 2, 4, 3, 0)])
+@pytest.mark.parametrize("pipe", [True, False], ids=["pipe", "onetick"])
+def test_run_ticks_fused_parity(gpu_available, monkeypatch, game, P, W, cd, d, pipe):
     """rb_run_ticks fuses consecutive steady-state ticks into one launch
-    (steady_kernel<G, CD>, CD <= 8; larger cd falls back to per-tick launches).
-    Chunks of ticks are compared bit-exactly with the oracle."""
+    (steady_kernel<G, CD>, CD <= 8; larger cd falls back to per-tick launches;
+    ex_game at odd CD >= 3 runs two ticks in flight, steady_pipe_kernel, unless
+    RB_STEADY_PIPE=0).  Chunks of ticks are compared bit-exactly with the oracle."""
     import torch
+    monkeypatch.setenv("RB_STEADY_PIPE", "1" if pipe else "0")
     S, T = 150, 120
     mask, dtype = (0xFFFFFFFF, np.uint32) if game == G.Game.STUB else ((1, np.uint8) if game == G.Game.STUB_ENUM
                                                                       else (0x0F, np.uint8))
@@ -405,10 +448,13 @@ def test_run_ticks_fused_parity(gpu_available, game, P, W, cd, d):
     assert t == T
 
 
-def test_run_ticks_fused_mismatch_and_corruption(gpu_available):
+@pytest.mark.parametrize("pipe", [True, False], ids=["pipe", "onetick"])
+def test_run_ticks_fused_mismatch_and_corruption(gpu_available, monkeypatch, pipe):
     """Mismatches detected inside a fused launch freeze exactly the sessions
-    (and report exactly the frames) that per-tick execution reports."""
+    (and report exactly the frames) that per-tick execution reports; with two
+    ticks in flight the tick after the failing one leaves no trace."""
     import torch
+    monkeypatch.setenv("RB_STEADY_PIPE", "1" if pipe else "0")
     S, P, cd = 64, 2, 7
     inputs = synth_inputs(S, P, 60, seed=4)
     sess, orc = make_pair(G.Game.EX_GAME, S, P, 8, cd, 2, checked=True)

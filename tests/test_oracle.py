@@ -159,3 +159,26 @@ def test_sincos_in_range_evaluation_equals_glibc(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout
     assert r.stdout.startswith("1087373312 floats, 0 mismatches")
+
+
+def test_optimized_cpu_baseline_matches_oracle():
+    # bench.py's second CPU baseline (oracle/soa_baseline.cpp, kind "optimized")
+    # must do the same work as the port: same live states and display checksums
+    # as the oracle's SyncTestSession + ex_game after T ticks, no mismatches.
+    from ggrs_amd.session import decode_ex_game
+    for P, cd, d, W, T in [(2, 7, 2, 8, 260), (3, 2, 0, 8, 90), (4, 7, 2, 8, 150), (2, 0, 1, 8, 40), (1, 5, 3, 9, 70)]:
+        S = 37
+        inputs = synth_inputs(S, P, T)
+        st, cs, ne = O.soa_exgame_run(P, cd, d, W, inputs)
+        assert ne == 0
+        b = O.OracleBatch(O.EX_GAME, P, W, cd, d, S)
+        for t in range(T):
+            for h in range(P):
+                b.add_local_input(h, inputs[t, h])
+            k, _ = b.advance()
+            assert (k == 0).all()
+        img, ocs, _ = b.read_live()
+        f = decode_ex_game(img, P)
+        want = np.concatenate([f["positions"], f["velocities"], f["rotations"][..., None]], -1)
+        np.testing.assert_array_equal(st.view(np.uint32), want.astype(np.float32).view(np.uint32))
+        np.testing.assert_array_equal(cs.astype(np.uint64), ocs)

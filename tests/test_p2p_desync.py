@@ -250,3 +250,83 @@ def test_gpu_queue_overflow_panic_inside_fused_launches(gpu_available):
         np.testing.assert_array_equal(g.frames()[0], orc.frames()[0])
         np.testing.assert_array_equal(g.read_live()[live], orc.read_live()[0][live])
     assert g.counters()[2] == victims.sum()
+
+
+# ---------------------------------------------------------------------------- RCCL at world size 1
+@pytest.mark.gpu
+def test_gpu_rccl_world1_report_allgather_and_p2p_exchange(gpu_available):
+    # The north-star collective executed on the device with the nccl (= RCCL)
+    # backend: SyncTest desync reports (rb_export_checksum_report ->
+    # shard.gather_reports, messages.rs:75-79) and the P2P ChecksumReport
+    # exchange (rb_p2p_take_checksum_reports -> shard.exchange_checksum_reports
+    # -> rb_p2p_receive_checksum_reports, p2p_session.rs:873-928), at world size 1:
+    # what comes back is what went in, and the peers fed through the collective
+    # raise exactly the oracle's DesyncDetected events.
+    import socket
+
+    import torch
+    import torch.distributed as dist
+
+    from ggrs_amd import shard
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    import os
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        assert dist.get_backend() == "nccl"
+        # SyncTest reports through the all-gather
+        S, T = 300, 20
+        inputs = G.synth_inputs(S, P, T)
+        sess = (G.SessionBuilder(G.Game.EX_GAME, num_sessions=S, device=0).with_num_players(P)
+                .with_check_distance(7).with_input_delay(2).with_checked_mismatches(False).start_synctest_session())
+        sess.run_ticks(torch.from_numpy(inputs).to(dev))
+        rep = torch.full((S, shard.REPORT_WORDS), 7, dtype=torch.int64, device=dev)
+        sess.export_checksum_report(T - 1, rep)
+        g = shard.gather_reports(rep)
+        assert torch.equal(g, rep)
+        orc = O.OracleBatch(O.EX_GAME, P, 8, 7, 2, S)
+        for t in range(T):
+            for h in range(P):
+                orc.add_local_input(h, inputs[t, h])
+            orc.advance()
+        frames, _, _, cs = orc.read_cells()
+        w = int(np.nonzero(frames == T - 1)[0][0])
+        r = g.cpu().numpy()
+        np.testing.assert_array_equal(r[:, 0].view(np.uint64), cs[w][:, 0])
+        assert ((r[:, 2] & 0xFFFFFFFF) == T - 1).all() and ((r[:, 2] >> 32) == -1).all()
+        sess.close()
+        # P2P ChecksumReports through the all-gather, one corrupted session
+        S, T, d, interval = 96, 60, 2, 5
+        inputs, na, nb = networks(S, T, d, (0, 1))
+        oa, ob = oracle_peer(MASK_A, S, d, interval), oracle_peer(MASK_B, S, d, interval)
+        ga, gb = gpu_peer(MASK_A, S, d, interval), gpu_peer(MASK_B, S, d, interval)
+        tens = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+        di, ua, ra, ub, rb = tens(inputs), tens(na[0]), tens(na[1]), tens(nb[0]), tens(nb[1])
+        for t in range(T):
+            if t == 23:
+                oa.corrupt(40, 4 * P, 0x00100000)
+                ga.debug_corrupt(40, 4 * P, 0x00100000)
+            ga.run_ticks(di[t:t + 1], ua[t:t + 1], ra)
+            gb.run_ticks(di[t:t + 1], ub[t:t + 1], rb)
+            oracle_tick(oa, MASK_A, inputs, na, t)
+            oracle_tick(ob, MASK_B, inputs, nb, t)
+            exchange_oracle(oa, ob)
+            rep_a, rep_b = ga.take_checksum_reports(), gb.take_checksum_reports()
+            xa, xb = shard.exchange_checksum_reports(rep_a), shard.exchange_checksum_reports(rep_b)
+            assert xa.shape == (1,) + tuple(rep_a.shape) and torch.equal(xa[0], rep_a) and torch.equal(xb[0], rep_b)
+            ga.receive_checksum_reports(1, xb[0])
+            gb.receive_checksum_reports(0, xa[0])
+        for g_, o_ in ((ga, oa), (gb, ob)):
+            gn, gfr, *_ = g_.desync_events()
+            on, ofr, *_ = o_.desync_events(RB_P2P_EVENTS_KEPT)
+            np.testing.assert_array_equal(gn, on)
+            np.testing.assert_array_equal(gfr, ofr)
+        assert set(np.nonzero(ga.desync_events()[0])[0].tolist()) == {40}
+        ga.close()
+        gb.close()
+    finally:
+        dist.destroy_process_group()

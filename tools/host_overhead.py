@@ -1,10 +1,14 @@
-"""Where the driver's 20-step wall time goes: host call vs kernel vs sync (GPU box)."""
+"""Where the driver's 20-step wall time goes (GPU box): the run_ticks call on
+the host, the wall time to the end of a synchronize, and the kernel time from
+HIP events; with and without the profiling events, with device vs stream
+synchronize, and the floor of one trivial launch + synchronize."""
 import os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch
 import ggrs_amd as G
-S, P, cd, steps = 65536, 2, 7, 20
-T = 8 + 5 + steps * 12
+S, P, cd, steps = 65536, 2, 7, int(os.environ.get("STEPS", "20"))
+reps = 12
+T = 8 + 5 + steps * (4 * reps + 2)
 inputs = G.synth_inputs(S, P, T)
 dev = torch.device("cuda", 0)
 d = torch.from_numpy(inputs).to(dev)
@@ -12,19 +16,59 @@ stream = torch.cuda.Stream(device=dev)
 sess = (G.SessionBuilder(G.Game.EX_GAME, num_sessions=S, device=0).with_num_players(P).with_check_distance(cd)
         .with_input_delay(2).with_checked_mismatches(False).start_synctest_session())
 sess.set_stream(stream)
-with torch.cuda.stream(stream):
-    for t in range(13):
-        sess.run_ticks(d[t:t + 1])
-    torch.cuda.synchronize()
-    t = 13
-    for rep in range(10):
+t = 13
+
+
+def rows(label, prof, sync):
+    global t
+    out = []
+    for rep in range(reps):
         x = d[t:t + steps]
-        sess.profile_enable(True); sess.profile_take()
+        sess.profile_enable(prof)
+        sess.profile_take()
         t0 = time.perf_counter()
         sess.run_ticks(x)
         t1 = time.perf_counter()
-        torch.cuda.synchronize()
+        sync()
         t2 = time.perf_counter()
         ms, n = sess.profile_take()
-        print(f"call {1e6*(t1-t0):7.1f} us  wall {1e6*(t2-t0):7.1f} us  kernel {1e3*ms:7.1f} us")
+        out.append((1e6 * (t1 - t0), 1e6 * (t2 - t0), 1e3 * ms))
         t += steps
+    a = np.array(out[2:])
+    med = np.median(a, 0)
+    print(f"{label:34s} call {med[0]:7.1f} us  wall {med[1]:7.1f} us  kernel {med[2]:7.1f} us  "
+          f"(min wall {a[:, 1].min():.1f})", flush=True)
+
+
+with torch.cuda.stream(stream):
+    sess.run_ticks(d[0:13])
+    torch.cuda.synchronize()
+    rows("prof on, device sync", True, torch.cuda.synchronize)
+    rows("prof off, device sync", False, torch.cuda.synchronize)
+    rows("prof on, stream sync", True, stream.synchronize)
+    rows("prof off, stream sync", False, stream.synchronize)
+    # floor: one trivial kernel + synchronize on the same stream
+    z = torch.zeros(64, device=dev)
+    w = []
+    for _ in range(20):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        z.add_(1)
+        torch.cuda.synchronize()
+        w.append(1e6 * (time.perf_counter() - t0))
+    print(f"{'trivial torch launch + sync':34s} wall {np.median(w[2:]):7.1f} us", flush=True)
+    # per-tick launches (live play: one tick of inputs per call)
+    sess.profile_enable(True)
+    sess.profile_take()
+    torch.cuda.synchronize()
+    n1 = steps * 4
+    t0 = time.perf_counter()
+    for k in range(n1):
+        sess.run_ticks(d[t + k:t + k + 1])
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    ms, n = sess.profile_take()
+    print(f"{'one tick per call':34s} call {1e6*(t1-t0)/n1:7.1f} us/tick  wall {1e6*(t2-t0)/n1:7.1f} us/tick  "
+          f"kernel {1e3*ms/max(1,n):7.1f} us/tick", flush=True)
+sess.close()
