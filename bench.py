@@ -339,13 +339,17 @@ def bench_p2p(args):
     lo, hi = (int(x) for x in args.lag.split(","))
     T = args.warmup + args.steps
     mask = 0b1
+    brawler = args.game == "brawler"
+    imask = args.input_mask if args.input_mask is not None else (0xFF if brawler else 0x0F)
     g0, g1 = shard.shard_range(rank, world, S * world)
-    inputs, upto, rin = synth_network(g1 - g0, P, T, mask, args.remote_delay, lo, hi, seed=args.seed, first_session=g0)
+    inputs, upto, rin = synth_network(g1 - g0, P, T, mask, args.remote_delay, lo, hi, seed=args.seed, first_session=g0,
+                                      mask=imask)
     di, du, dr = (torch.from_numpy(a).to(dev) for a in (inputs, upto, rin))
-    b = (G.SessionBuilder(G.Game.EX_GAME, num_sessions=S, device=local).with_num_players(P)
-         .with_max_prediction_window(W).with_input_delay(args.input_delay).with_remote_input_delay(args.remote_delay)
-         .with_sparse_saving_mode(args.sparse_saving).with_block_size(args.block_size)
-         .with_speculative_fanout(args.fanout))
+    K = args.fanout_k
+    b = (G.SessionBuilder(G.Game.BRAWLER if brawler else G.Game.EX_GAME, num_sessions=S, device=local)
+         .with_num_players(P).with_max_prediction_window(W).with_input_delay(args.input_delay)
+         .with_remote_input_delay(args.remote_delay).with_sparse_saving_mode(args.sparse_saving)
+         .with_block_size(args.block_size).with_speculative_fanout(args.fanout, K))
     for h in range(P):
         b.add_player(PlayerType.Local if (mask >> h) & 1 else PlayerType.Remote, h)
     sess = b.start_p2p_session()
@@ -412,48 +416,53 @@ def bench_p2p(args):
         # 2 B checksum, 4 B frame tag per save), the inputs of every AdvanceFrame
         # (P bytes), and per session-tick the local input read + ring write, the
         # delivery watermark and one remote input read + ring write (8 B)
-        state = 4 * 5 * P
+        state = 4 * 256 * 8 if brawler else 4 * 5 * P
         bytes_rank = (adv / world * P + saves / world * (state + 6) + loads / world * state
                       + S * args.steps * 8)
         generic_fan = os.environ.get("RB_FANOUT_GENERIC", "0") not in ("", "0")
-        if args.fanout and generic_fan:  # fanout_kernel: per branch frame its cell + checksum stored and its
-            # inputs; per session-tick the base cell load and 16 branch states stored; per select the
+        if args.fanout and (generic_fan or brawler):  # fanout_kernel: per branch frame its cell + checksum stored
+            # and its inputs; per session-tick the base cell load and K branch states stored; per select the
             # selected cells read back
-            bytes_rank += branch / world * (state + 2 + P) + S * args.steps * state * 17 + selects / world * state
+            bytes_rank += branch / world * (state + 2 + P) + S * args.steps * state * (K + 1) + selects / world * state
         elif args.fanout:  # fanout_indep_kernel: the players not speculated on are simulated once per
             # session, so per presimulated frame 16 x (the speculated player's cell part + checksum + input)
             # + (P - 1) x (a player's cell part + input); per session-tick the base cell load and the final
             # states (16 speculated + P - 1 others); per select the selected cells read back
             ps = state // P
-            frames = branch / world / 16
-            bytes_rank += (frames * (16 * (ps + 2 + 1) + (P - 1) * (ps + 1)) + S * args.steps * (state + (16 + P - 1) * ps)
+            frames = branch / world / K
+            bytes_rank += (frames * (K * (ps + 2 + 1) + (P - 1) * (ps + 1)) + S * args.steps * (state + (K + P - 1) * ps)
                            + selects / world * state)
         avg_kernel_s = kernel_ms / 1e3 / max(1, launches)
-        cfg_key = (f"p2p ex_game P={P} W={W} d={args.input_delay} rd={args.remote_delay} lag={lo},{hi} S={S}"
-                   + (" sparse" if args.sparse_saving else "") + (" fanout" if args.fanout else "")
+        cfg_key = (f"p2p {args.game} P={P} W={W} d={args.input_delay} rd={args.remote_delay} lag={lo},{hi} S={S}"
+                   + (" sparse" if args.sparse_saving else "") + (f" fanout{'' if K == 16 else K}" if args.fanout else "")
                    + (" wire" if args.wire else ""))
+        gname = f"Brawler<{P}>" if brawler else f"ExGame<{P},true>"
         roofline = roofline_block(bytes_rank / max(1, launches), avg_kernel_s, args.steps / max(1, launches), launches,
-                                  f"p2p_kernel<ExGame<{P},true>>" + ((" + fanout_kernel (per tick)" if generic_fan
-                                                                      else " + fanout_indep_kernel (per tick)")
-                                                                     if args.fanout
-                                                                     else " (fused P2P ticks)"),
+                                  f"p2p_kernel<{gname}>" + ((" + fanout_kernel (per tick)" if generic_fan or brawler
+                                                             else " + fanout_indep_kernel (per tick)")
+                                                            if args.fanout
+                                                            else " (fused P2P ticks)"),
                                   pmc_profile(cfg_key), "algorithmic: cells loaded/saved, inputs, deliveries")
         line = {
             "metric": "P2P session-frames simulated/sec (node), rollback to the first mispredicted frame",
             "value": adv / elapsed, "unit": "session-frames/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": f"ex_game P2PSession x {S} sessions/GPU, {P} players (handle 0 local), "
+            "config": {"workload": f"{args.game} P2PSession x {S} sessions/GPU, {P} players (handle 0 local), "
                                    f"max_prediction {W}, input delay {args.input_delay}, remote delay "
                                    f"{args.remote_delay}, network lag {lo}-{hi} frames"
                                    + (", sparse saving" if args.sparse_saving else "")
-                                   + (", speculative fan-out 16 candidates/frame" if args.fanout else "")
+                                   + (f", speculative fan-out {K} candidates/frame" if args.fanout else "")
+                                   + f", inputs masked 0x{imask:X}"
                                    + (", inputs delivered as packets (device encode + decode per tick)"
                                       if args.wire else ""),
                        "sessions_per_gpu": S, "total_sessions": S * world,
                        "advance_frames_per_session_tick": adv / (S * world * args.steps),
                        "rollbacks_per_session_tick": (loads + selects) / (S * world * args.steps),
-                       "speculative": ({"branches": 16, "selects": selects, "loads": loads,
+                       "speculative": ({"branches": K, "alphabet": 16 if not brawler else 256,
+                                        "candidates": "whole alphabet" if (not brawler and K >= 16) else
+                                                      "K most recently confirmed distinct inputs, then smallest values",
+                                        "selects": selects, "loads": loads,
                                         "select_fraction": selects / max(1, selects + loads),
                                         "branch_frames_per_s": branch / elapsed}
                                        if args.fanout else None),
@@ -467,13 +476,17 @@ def bench_p2p(args):
             # pattern) on the same arrays: same inputs, same delivery schedule, same rollbacks
             from oracle import oracle as O
             threads = cpu_threads()
-            secs, cadv, nerr = O.bench_p2p_exgame(P, W, args.input_delay, mask, args.remote_delay, inputs, upto, rin,
-                                                  args.warmup, threads)
+            cs_ = min(S, 8192) if brawler else S  # the brawler port: a bounded sample of sessions
+            secs, cadv, nerr = O.bench_p2p_exgame(P, W, args.input_delay, mask, args.remote_delay,
+                                                  np.ascontiguousarray(inputs[:, :, :cs_]),
+                                                  np.ascontiguousarray(upto[:, :, :cs_]),
+                                                  np.ascontiguousarray(rin[:, :, :cs_]), args.warmup, threads,
+                                                  game=O.BRAWLER if brawler else O.EX_GAME)
             line["cpu_baseline"] = {
                 "value": cadv / secs, "unit": "session-frames/s", **cpu_info(threads), "kind": "port",
-                "sample": f"the full workload ({S} sessions x {args.steps} timed ticks, {cadv} AdvanceFrames) through "
-                          f"the C++ restatement of P2PSession rollback (no fan-out: the reference has none), "
-                          f"{threads} host threads, {secs:.2f} s wall, {nerr} errors"}
+                "sample": f"{cs_} of the {S} sessions x {args.steps} timed ticks ({cadv} AdvanceFrames), same inputs "
+                          f"and deliveries, through the C++ restatement of P2PSession rollback (no fan-out: the "
+                          f"reference has none), {threads} host threads, {secs:.2f} s wall, {nerr} errors"}
         print(json.dumps(line), flush=True)
     sess.close()
     if world > 1:
@@ -516,8 +529,13 @@ def main():
                     help="p2p: remote inputs travel as packets each tick: device encode (send_pending_output) + "
                          "decode (on_input) into the delivery tensors, then one P2P tick")
     ap.add_argument("--fanout", action="store_true",
-                    help="p2p: speculative fan-out, 16 candidate inputs per session per tick (BASELINE configs[3]; "
-                         "use with --num-players 4)")
+                    help="p2p: speculative fan-out, --fanout-k candidate inputs per session per tick (BASELINE "
+                         "configs[3]; use with --num-players 4)")
+    ap.add_argument("--fanout-k", type=int, default=16,
+                    help="p2p --fanout: candidates per session (1..16): ex_game's whole alphabet at 16, else the "
+                         "most likely K")
+    ap.add_argument("--input-mask", type=lambda x: int(x, 0), default=None,
+                    help="synthetic input bits (default 0x0F ex_game, 0xFF brawler)")
     ap.add_argument("--audit-sessions", type=int, default=64,
                     help="N>1: each rank also simulates this many sessions of the next rank's shard; after every "
                          "report all-gather the owner's checksums are compared with the replica's (DesyncDetected)")
@@ -652,20 +670,30 @@ def main():
         # time (ex_game_synctest.rs:50-61), so each tick is its own call and launch.
         rt = None
         if RT:
+            # wall time of RT one-tick calls without profiling events, then the kernel time of each
+            # launch from events over RT more (an event pair per launch adds host time of its own)
             t_rt = warm + args.steps
-            sess.profile_take()
+            half = RT // 2
+            sess.profile_enable(False)
             torch.cuda.synchronize()
             r0 = time.perf_counter()
-            for k in range(RT):
+            for k in range(half):
                 sess.run_ticks(dinputs[t_rt + k:t_rt + k + 1])
             torch.cuda.synchronize()
             rt_wall = time.perf_counter() - r0
+            sess.profile_enable(True)
+            sess.profile_take()
+            for k in range(half, RT):
+                sess.run_ticks(dinputs[t_rt + k:t_rt + k + 1])
+            torch.cuda.synchronize()
             rt_kernel_ms, rt_ticks = sess.profile_take()
-            rt = {"ticks": RT, "ticks_per_call": 1, "wall_us_per_tick": rt_wall / RT * 1e6,
+            rt = {"ticks": RT, "ticks_per_call": 1, "wall_us_per_tick": rt_wall / half * 1e6,
                   "kernel_us_per_tick": rt_kernel_ms * 1e3 / max(1, rt_ticks),
-                  "max_ticks_per_s": RT / rt_wall, "headroom_60hz": RT / rt_wall / 60.0,
-                  "note": "one tick per rb_run_ticks call (live play), all sessions of this GPU; headroom = "
-                          "sustainable ticks/s / 60"}
+                  "max_ticks_per_s": half / rt_wall, "headroom_60hz": half / rt_wall / 60.0,
+                  "tick_latency_us": rt_kernel_ms * 1e3 / max(1, rt_ticks),
+                  "note": "one tick per rb_run_ticks call (live play, inputs arriving per tick), all sessions of "
+                          "this GPU: wall over the first half (no events), kernel time from HIP events over the "
+                          "second; headroom = sustainable ticks/s / 60"}
 
     nfail = int((sess.mismatches()[:S] != G.NULL_FRAME).sum())  # owned sessions only
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)

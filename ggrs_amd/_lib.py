@@ -74,7 +74,8 @@ class RbP2PConfig(ctypes.Structure):
         ("flags", ctypes.c_uint32),
         ("block_size", ctypes.c_uint32),
         ("desync_interval", ctypes.c_int32),
-        ("reserved", ctypes.c_uint32 * 3),
+        ("fanout_candidates", ctypes.c_int32),
+        ("reserved", ctypes.c_uint32 * 2),
     ]
 
 

@@ -128,7 +128,7 @@ struct rb_batch {
   // fused launch ran ticks whose host bookkeeping then failed): every later
   // call fails with RB_PANIC, as the reference process would have stopped.
   std::string poisoned;
-  bool pipe = true;  // fused steady ticks with two ticks in flight (RB_STEADY_PIPE=0 at create: one at a time)
+  bool pipe = false;  // fused steady ticks with two ticks in flight (RB_STEADY_PIPE=1 at create; A/B, tests)
 };
 
 namespace {

@@ -74,6 +74,7 @@ struct ExGame {
   static constexpr int kPlayersPerLane = kSplit ? 1 : P;
   static constexpr int NWL = 5 * kPlayersPerLane;  // per player: x, y, vx, vy, rot
   static constexpr int kInputBytes = 1;
+  static constexpr uint32_t kInputAlphabet = 16;  // the 4 input flag bits (ex_game.rs:16-19): the fan-out's candidates
   static constexpr int kImageBytes = 36 + 20 * P;  // bincode 1.3 image of State (ex_game.rs:224-231)
   static_assert(255 * kImageBytes * (kImageBytes + 1) / 2 < (1 << 24), "fl16_finish needs sums < 2^24");
   static constexpr bool kDisplay = true;           // Game::last_checksum / periodic_checksum

@@ -163,7 +163,8 @@ __device__ __forceinline__ void advance_fast(uint32_t (&w)[G::NWL], const Pr& pr
   if constexpr (HasFast<G>::value) G::advance_prepared_fast(w, pr, k, special);
 }
 #ifndef RB_FAST_ADVANCE
-#define RB_FAST_ADVANCE 1  // 0: the branchy AdvanceFrame everywhere (A/B builds, tools/mkvar.sh)
+#define RB_FAST_ADVANCE 0  // 1: the branch-free AdvanceFrame with redo (A/B builds, tools/mkvar.sh): measured
+                           // neutral on p2p_kernel (191 vs 191 us per 50 ticks, round 3)
 #endif
 // One AdvanceFrame{inputs} (State::advance, ex_game.rs:259-321) for the
 // kernels that run frames one at a time (tick_kernel, p2p_kernel, the
@@ -392,7 +393,8 @@ struct DecSel<G, true> {
 template <class G>
 using DecOf = typename DecSel<G>::type;
 #ifndef RB_STEADY_FAST
-#define RB_STEADY_FAST 1  // 0: the branchy form on every tick (A/B builds, tools/mkvar.sh)
+#define RB_STEADY_FAST 0  // 1: the branch-free form with the tick redo (A/B builds, tools/mkvar.sh): measured
+                          // slower, 269 vs 220 us per 50 ticks (round 3)
 #endif
 
 // kExp: attribution experiments (RunParams::debug knobs, tools/exp_steady.py);
@@ -755,9 +757,9 @@ struct GameOpsT final : GameOps {
       // the snapshot ring in LDS (p2p_lds_cell_bytes) for launches of many ticks: it is copied in and
       // written back whole, which short launches (the wire path's one tick per launch) do not repay
       if (p2p_lds_cells<G>(p.W, block) && p.T >= kLdsCellsMinTicks) {
-        // lane-asynchronous ticks on the plain path unless the batch asked for lock-step ticks
-        auto k = (!kSparse && !p.sync_ticks) ? p2p_kernel<G, kSpec, kSparse, kNet, true, !kSparse>
-                                             : p2p_kernel<G, kSpec, kSparse, kNet, true, false>;
+        // lane-asynchronous ticks (plain path and sparse saving) unless the batch asked for lock-step ticks
+        auto k = !p.sync_ticks ? p2p_kernel<G, kSpec, kSparse, kNet, true, true>
+                               : p2p_kernel<G, kSpec, kSparse, kNet, true, false>;
         lds += p2p_lds_cell_bytes<G>(block, p.W);
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                            static_cast<int>(lds));
@@ -782,7 +784,8 @@ struct GameOpsT final : GameOps {
     if (kFanout && p.spec_on) return launch_p2p_as<kFanout, false, false>(p, grid, block, st);
     return launch_p2p_as<false, false, false>(p, grid, block, st);
   }
-  static constexpr bool kFanout = G::kLanes > 1 && G::kLanes <= 4;
+  // fan-out: one lane per player (ex_game) or one wave per session (the brawler), 1-byte inputs
+  static constexpr bool kFanout = ((G::kLanes > 1 && G::kLanes <= 4) || G::kLanes == 64) && G::kInputBytes == 1;
   hipError_t launch_fanout(const FanParams& p, int block, hipStream_t st) const override {
     if constexpr (kFanout && IndepPlayers<G>::value) {  // the players the fan-out does not speculate on, once
       if (!p.fan_generic) {

@@ -61,12 +61,126 @@ constexpr int32_t kP2PStatusOk = 0, kP2PStatusThreshold = 1, kP2PStatusPanic = 1
 // executed work: AdvanceFrames, SaveGameStates, LoadGameStates, rollbacks
 // replaced by a speculative branch select, branch frames presimulated
 enum : int { ST_ADV = 0, ST_SAVE = 1, ST_LOAD = 2, ST_SELECT = 3, ST_BRANCH = 4, ST_COUNT = 5 };
-// Speculative fan-out: branch k holds candidate input k for one remote player
-// over its unconfirmed frames (the full 4-bit ex_game alphabet).
+// Speculative fan-out: branch k holds candidate input cand[k] for one remote
+// player over its unconfirmed frames.  Up to kSpecBranches
+// candidates: the game's whole input alphabet when it has at most that many
+// values (ex_game's 4 bits: cand[k] = k), else the K most likely values
+// (fan_candidates below).
 constexpr int kSpecBranches = 16;
 // spec_meta rows: first speculated frame (base), frame the branch states are at
-// (end), speculated handle, valid flag
-enum : int { SM_BASE = 0, SM_END = 1, SM_PLAYER = 2, SM_VALID = 3, SM_COUNT = 4 };
+// (end), speculated handle, valid flag, then the 16 candidate inputs (1-byte
+// inputs, 4 per row; 0xFF..: no branch) the branches presimulated
+enum : int { SM_BASE = 0, SM_END = 1, SM_PLAYER = 2, SM_VALID = 3, SM_CAND = 4, SM_COUNT = 8 };
+
+// The input alphabet a game's fan-out draws candidates from: G::kInputAlphabet,
+// else every value of its Input.
+template <class G, class = void>
+struct InputAlphabet {
+  static constexpr uint32_t value = G::kInputBytes >= 2 ? 0xFFFFFFFFu : 256u;
+};
+template <class G>
+struct InputAlphabet<G, std::void_t<decltype(G::kInputAlphabet)>> {
+  static constexpr uint32_t value = G::kInputAlphabet;
+};
+
+// The K candidate inputs of the speculated player h (K <= kSpecBranches,
+// 1-byte inputs): with an alphabet of at most K values, the alphabet in value
+// order (branch k = input k); otherwise the most recently confirmed distinct
+// values, newest first (the reference's prediction, repeat-last
+// (input_queue.rs:126-140), is candidate 0), looking back at most 32 frames
+// from the last added one, then the smallest values not yet taken.  Packed 4
+// per word, unused slots 0xFF with `n` = K.
+template <class R>
+__device__ __forceinline__ void fan_candidates(const R& ring, int h, unsigned s, int32_t la, uint32_t alphabet, int K,
+                                               uint32_t (&packed)[4]) {
+  uint32_t cand[kSpecBranches];
+  if (alphabet <= static_cast<uint32_t>(K)) {
+#pragma unroll
+    for (int i = 0; i < kSpecBranches; ++i) cand[i] = static_cast<uint32_t>(i) < alphabet ? static_cast<uint32_t>(i) : 0xFFu;
+  } else {
+    uint64_t present[4] = {0ull, 0ull, 0ull, 0ull};  // values taken (alphabet <= 256)
+    int n = 0;
+#pragma unroll
+    for (int i = 0; i < kSpecBranches; ++i) cand[i] = 0xFFu;
+    constexpr int kBack = 32;
+    uint32_t hist[kBack];
+#pragma unroll
+    for (int d = 0; d < kBack; ++d) hist[d] = ring.get(max(la - d, 0), h, s);  // independent loads first
+#pragma unroll
+    for (int d = 0; d < kBack; ++d) {
+      const uint32_t v = hist[d] & 0xFFu;
+      const uint64_t word = present[v >> 6 & 3];
+      const bool take = la - d >= 0 && n < K && !((word >> (v & 63)) & 1ull);
+#pragma unroll
+      for (int i = 0; i < kSpecBranches; ++i) cand[i] = (take && i == n) ? v : cand[i];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) present[q] |= (take && q == static_cast<int>(v >> 6)) ? (1ull << (v & 63)) : 0ull;
+      n += take ? 1 : 0;
+    }
+    // fill: the smallest values of the alphabet not taken
+#pragma unroll
+    for (int i = 0; i < kSpecBranches; ++i) {
+      if (i >= K) break;
+      int q = 0;
+      while (q < 3 && present[q] == ~0ull) ++q;
+      const uint32_t x = static_cast<uint32_t>(q * 64 + __builtin_ctzll(~present[q]));
+      const bool fill = i >= n && x < alphabet;
+      cand[i] = fill ? x : cand[i];
+#pragma unroll
+      for (int w = 0; w < 4; ++w) present[w] |= (fill && w == q) ? (1ull << (x & 63)) : 0ull;
+    }
+  }
+#pragma unroll
+  for (int w = 0; w < 4; ++w)
+    packed[w] = (cand[4 * w] & 0xFFu) | ((cand[4 * w + 1] & 0xFFu) << 8) | ((cand[4 * w + 2] & 0xFFu) << 16) |
+                ((cand[4 * w + 3] & 0xFFu) << 24);
+}
+// The inputs a fan-out lane's player feeds its branch frames base .. base+7
+// (confirmed ones from the ring, the repeat-last prediction past the last
+// added frame), all loaded before the frame loop: inside it each frame's ring
+// read would wait a global-memory round trip on the dependent chain.
+constexpr int kFanPre = 8;
+template <class R>
+__device__ __forceinline__ void fan_prefetch(const R& ring, int h, unsigned s, int32_t base, int32_t cur, bool confirmed_all,
+                                             int32_t la_h, uint32_t pred, uint32_t (&vin)[kFanPre]) {
+  uint32_t raw[kFanPre];
+#pragma unroll
+  for (int j = 0; j < kFanPre; ++j) raw[j] = ring.get(min(base + j, max(cur - 1, base)), h, s);
+#pragma unroll
+  for (int j = 0; j < kFanPre; ++j) {
+    const int32_t f = base + j;
+    vin[j] = (confirmed_all || (la_h != kNullFrame && f <= la_h)) ? raw[j] : pred;
+  }
+}
+// the prefetched window as 8 bytes: input of frame base + j = byte j (1-byte inputs)
+__device__ __forceinline__ uint64_t fan_pack(const uint32_t (&vin)[kFanPre]) {
+  uint64_t x = 0;
+#pragma unroll
+  for (int j = 0; j < kFanPre; ++j) x |= static_cast<uint64_t>(vin[j] & 0xFFu) << (8 * j);
+  return x;
+}
+__device__ __forceinline__ uint32_t fan_input(uint64_t packed, int j) {
+  return static_cast<uint32_t>(packed >> (8 * j)) & 0xFFu;
+}
+// The slot of candidate value v among the first K packed candidates, or -1:
+// a zero-byte search over (packed ^ v in every byte) (the lowest zero byte
+// of x is the lowest set bit of (x - 0x01..) & ~x & 0x80..).
+__device__ __forceinline__ int32_t cand_find(const uint32_t (&packed)[4], uint32_t v, int K) {
+  const uint64_t rep = 0x0101010101010101ull * (v & 0xFFu);
+  const uint64_t lo = (static_cast<uint64_t>(packed[1]) << 32 | packed[0]) ^ rep;
+  const uint64_t hi = (static_cast<uint64_t>(packed[3]) << 32 | packed[2]) ^ rep;
+  const uint64_t zl = (lo - 0x0101010101010101ull) & ~lo & 0x8080808080808080ull;
+  const uint64_t zh = (hi - 0x0101010101010101ull) & ~hi & 0x8080808080808080ull;
+  const int32_t i = zl ? static_cast<int32_t>(__builtin_ctzll(zl) >> 3)
+                       : (zh ? 8 + static_cast<int32_t>(__builtin_ctzll(zh) >> 3) : kSpecBranches);
+  return (i < K && v <= 0xFFu) ? i : -1;
+}
+__device__ __forceinline__ uint32_t cand_at(const uint32_t (&packed)[4], int k) {
+  uint32_t w = packed[0];
+#pragma unroll
+  for (int q = 1; q < 4; ++q) w = (k >> 2) == q ? packed[q] : w;
+  return (w >> (8 * (k & 3))) & 0xFFu;
+}
 
 // ---------------------------------------------------------------------------
 // Desync detection (p2p_session.rs:154-157, 313-316, 873-928; the UdpProtocol
@@ -135,6 +249,7 @@ struct P2PParams {
   const int32_t* spec_meta;    // [SM_COUNT][Spad]
   int32_t spec_on;
   int32_t fan_generic;  // the branches were left by fanout_kernel, not fanout_indep_kernel
+  int32_t fan_k;        // candidates (branches) per session, <= kSpecBranches
   const uint8_t* local_in;  // tick t, handle h: local_in + t * local_stride + (h * S + s) * IB
   int64_t local_stride;
   const int32_t* upto;      // tick t, handle h: upto[t * upto_stride + h * S + s]
@@ -430,7 +545,16 @@ __device__ __forceinline__ uint32_t q_input(DevQueue& q, const R& r, int h, unsi
 // The speculative fan-out runs fanout_indep_kernel for games whose players move
 // independently, unless the batch asks for the generic fanout_kernel
 // (fan_generic: RB_FANOUT_GENERIC=1 at create, for A/B and tests).
-constexpr int kIndepLanes = 32;  // lanes per session in fanout_indep_kernel
+// fanout_indep_kernel's spec columns per session: the 16 branches of the
+// speculated player, then the P - 1 other players (handle order, skipping the
+// speculated one), with no padding between sessions: every 128-byte line of a
+// spec plane is written whole (a 32-column block per session left 13 of 32
+// columns unwritten at P = 4 and its partial lines cost 1.6x the algorithmic
+// store bytes, round 2's C4 profile)
+template <class G>
+constexpr int indep_cols() {
+  return kSpecBranches + G::kPlayers - 1;
+}
 
 // kSpec / kSparse / kNet: the fan-out select, sparse saving and the
 // network-fed bookkeeping (desync detection, peers' connect-status reports)
@@ -458,7 +582,7 @@ constexpr int kIndepLanes = 32;  // lanes per session in fanout_indep_kernel
 // which touch neither the state nor the cells.
 template <class G, bool kSpec, bool kSparse, bool kNet, bool kLdsC, bool kAsync>
 __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
-  static_assert(!kAsync || (kLdsC && !kSparse && !kSpec && !kNet), "lane-asynchronous ticks: plain path, LDS cells");
+  static_assert(!kAsync || (kLdsC && !kSpec && !kNet), "lane-asynchronous ticks: plain or sparse path, LDS cells");
   using InRec = typename G::InRec;
   using CS = typename G::CS;
   constexpr int NW = G::NWL;
@@ -534,11 +658,14 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
   load_words<NW>(p.live, static_cast<int>(Gpad), static_cast<int>(g), w);
   // the fan-out's branch metadata (written between launches), with the state loads
   [[maybe_unused]] int32_t sm_valid = 0, sm_end = 0, sm_base = 0, sm_player = 0;
+  [[maybe_unused]] uint32_t sm_cand[4] = {0u, 0u, 0u, 0u};
   if constexpr (kSpec) {
     sm_valid = p.spec_meta[SM_VALID * Spad + s];
     sm_end = p.spec_meta[SM_END * Spad + s];
     sm_base = p.spec_meta[SM_BASE * Spad + s];
     sm_player = p.spec_meta[SM_PLAYER * Spad + s];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) sm_cand[q] = static_cast<uint32_t>(p.spec_meta[(SM_CAND + q) * Spad + s]);
   }
   if (panicked) return;
   // LDS queue: the HBM frames this launch can read.  Reads are of frames
@@ -716,8 +843,10 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
         for (int32_t f = base + 1; f <= q[j].last_added && f < cur; ++f) ok &= ring.get(f, h, s) == k;
       }
     }
-    // the lane that owns the speculated player found k; share it with the group
-    int32_t kk = (kSplit ? lane == rs : true) ? static_cast<int32_t>(k) : -1;
+    // the lane that owns the speculated player found the held value k; its branch is the candidate
+    // slot holding k (none: no branch presimulated it); share it with the group
+    int32_t kk = cand_find(sm_cand, k, p.fan_k);
+    kk = (kSplit ? lane == rs : true) ? kk : -1;
     kk = -group_min<L>(-kk);  // max over the group
     ok = group_min<L>(ok ? 1 : 0) == 1;
     if (!ok || kk < 0 || kk >= kSpecBranches) return false;
@@ -729,13 +858,16 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     // players (fanout_indep_kernel) column s * 32 + kk of the speculated player's lane, s * 32 + 16 + lane
     // of any other player's (one trajectory for all branches), planes Spad * 32 wide
     const bool indep = IndepPlayers<G>::value && !p.fan_generic;
-    const unsigned Gs = indep ? Spad * kIndepLanes : Gpad * kSpecBranches;
+    constexpr unsigned LS = static_cast<unsigned>(indep_cols<G>());
+    const unsigned Gs = indep ? Spad * LS : Gpad * kSpecBranches;
     const unsigned col = !indep ? (s * kSpecBranches + static_cast<unsigned>(kk)) * L + lane
-                                : s * kIndepLanes + (lane == rs ? static_cast<unsigned>(kk) : kSpecBranches + lane);
+                                : s * LS + (lane == rs ? static_cast<unsigned>(kk)
+                                                       : kSpecBranches + static_cast<unsigned>(lane < rs ? lane : lane - 1));
     const CS* __restrict__ scs = reinterpret_cast<const CS*>(p.spec_cs);
-    // the padding lane of a 4-lane group (P = 3) holds no player: no branch column was written
-    // for it (fanout_indep_kernel), so it keeps its own words; nothing observes them
-    const bool real = !kSplit || lane < P;
+    // the padding lane of a 4-lane group (P = 3, one lane per player) holds no player: no branch
+    // column was written for it (fanout_indep_kernel), so it keeps its own words; nothing observes
+    // them.  (A wave-per-session game holds state in every lane.)
+    const bool real = !kSplit || L == 64 || lane < P;
     for (int32_t f = base + 1; f < cur; ++f) {  // the cells adjust would have saved
       const unsigned slot = static_cast<unsigned>(f % W);
       if (real) {
@@ -1074,6 +1206,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     int t = 0, count = 0, i = 0;
     int32_t confirmed = 0;
     bool inres = false, stopped = false;
+    [[maybe_unused]] bool checked = false;  // kSparse: check_last_saved_state already ran this tick
     [[maybe_unused]] uint32_t iters = 0;
     while (inres || (!stopped && t < p.T)) {
       if constexpr (RB_P2P_EXP & 4) ++iters;
@@ -1093,18 +1226,34 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
             disc_frame = kNullFrame;
           }
           if (status == kP2PStatusPanic) stopped = true;
-          else inres = true, i = 0;
+          else inres = true, i = 0, checked = false;
+        }
+      }
+      if constexpr (kSparse) {
+        // check_last_saved_state (p2p_session.rs:778-802), once the first rollback is done: a save of
+        // the current frame, or a second rollback from the last saved frame (its frames follow)
+        if (inres && i >= count && !checked) {
+          checked = true;
+          if (cur - last_saved >= W) {
+            if (confirmed >= cur) {
+              save(cur);
+            } else {
+              count = adjust_begin(last_saved);
+              i = 0;
+              if (status == kP2PStatusPanic) stopped = true, inres = false;
+            }
+          }
         }
       }
       if (inres) {
         bool save_now, finish = false;
-        if (i < count) {  // resimulated frame i of adjust_gamestate
-          save_now = i > 0;
+        if (i < count) {  // resimulated frame i of adjust_gamestate (sparse: the frame min_confirmed is saved)
+          save_now = kSparse ? cur == confirmed : i > 0;
           ++i;
         } else {  // the rest of advance_frame, add_local_input, then the tick's new frame
           set_last_confirmed(confirmed);
           add_local();
-          save_now = true;  // rollback_and_save's SaveGameState of the current frame
+          save_now = !kSparse;  // rollback_and_save's SaveGameState of the current frame (not with sparse saving)
           finish = true;
           inres = false;
         }
@@ -1206,6 +1355,7 @@ struct FanParams {
   int32_t S, Spad, W;
   uint32_t local_mask;
   int32_t fan_generic;  // fanout_kernel even for independent players
+  int32_t fan_k;        // candidates (branches) per session, <= kSpecBranches
 };
 
 template <class G>
@@ -1215,7 +1365,7 @@ __global__ void __launch_bounds__(256) fanout_kernel(const FanParams p) {
   constexpr int NW = G::NWL;
   constexpr int L = G::kLanes;
   constexpr int P = G::kPlayers, IB = G::kInputBytes;
-  static_assert(L > 1 || P == 1, "fan-out runs with one lane per player");
+  static_assert(L > 1 || P == 1, "fan-out runs with one lane per player (or a wave per session)");
   constexpr int LS = kSpecBranches * L;  // lanes per session
   const unsigned g = blockIdx.x * blockDim.x + threadIdx.x;
   const unsigned s = g / LS;
@@ -1247,13 +1397,18 @@ __global__ void __launch_bounds__(256) fanout_kernel(const FanParams p) {
   const int32_t base = la_rs + 1;  // first unconfirmed frame of the speculated player
   const bool valid = p.status[s] != kP2PStatusPanic && !any_disc && rs >= 0 && base < cur && base + W > cur && base >= 0 &&
                      p.tag[static_cast<unsigned>(base % W) * Spad + s] == base;
+  uint32_t cand[4];  // the speculated player's candidates (every lane of the session computes the same)
+  fan_candidates(ring, max(rs, 0), s, la_rs, InputAlphabet<G>::value, p.fan_k, cand);
   if (k == 0 && lane == 0) {
     p.spec_meta[SM_BASE * Spad + s] = base;
     p.spec_meta[SM_END * Spad + s] = cur;
     p.spec_meta[SM_PLAYER * Spad + s] = rs;
     p.spec_meta[SM_VALID * Spad + s] = valid ? 1 : 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) p.spec_meta[(SM_CAND + q) * Spad + s] = static_cast<int32_t>(cand[q]);
   }
-  if (!valid) return;  // session-uniform: the whole group leaves
+  if (!valid || k >= p.fan_k) return;  // session-uniform (branch-uniform): the whole group leaves
+  const uint32_t ck = cand_at(cand, k);
   const unsigned gl = s * L + lane;  // this lane's column in the session-major planes
   uint32_t w[NW];
   load_words<NW>(p.snap + static_cast<unsigned>(base % W) * NW * Gpad, static_cast<int>(Gpad), static_cast<int>(gl), w);
@@ -1263,6 +1418,9 @@ __global__ void __launch_bounds__(256) fanout_kernel(const FanParams p) {
   const bool local = active && ((p.local_mask >> h) & 1u);
   const int32_t la_h = active ? qrow(QF_LAST_ADDED, h) : kNullFrame;
   const uint32_t pred = (!active || la_h == kNullFrame) ? 0u : ring.get(la_h, h, s);
+  uint32_t vin[kFanPre];
+  fan_prefetch(ring, active ? h : 0, s, base, cur, local, la_h, pred, vin);
+  const uint64_t vpk = fan_pack(vin);
   CS* __restrict__ cs = reinterpret_cast<CS*>(p.spec_cs);
   uint32_t frames = 0;
   for (int32_t f = base; f < cur; ++f) {
@@ -1275,7 +1433,9 @@ __global__ void __launch_bounds__(256) fanout_kernel(const FanParams p) {
     }
     uint32_t v = 0;
     if (active) {
-      if (h == rs) v = static_cast<uint32_t>(k);
+      const int j = f - base;
+      if (h == rs) v = ck;
+      else if (j < kFanPre) v = fan_input(vpk, j);
       else if (local || (la_h != kNullFrame && f <= la_h)) v = ring.get(f, h, s);  // Confirmed
       else v = pred;  // repeat-last prediction (blank before the first input)
     }
@@ -1284,7 +1444,7 @@ __global__ void __launch_bounds__(256) fanout_kernel(const FanParams p) {
     ++frames;
   }
   store_words<NW>(p.spec_state, static_cast<int>(Gs), static_cast<int>(g), w);
-  if (k == 0 && lane == 0) p.stats[ST_BRANCH * Spad + s] += static_cast<unsigned long long>(frames) * kSpecBranches;
+  if (k == 0 && lane == 0) p.stats[ST_BRANCH * Spad + s] += static_cast<unsigned long long>(frames) * p.fan_k;
 }
 
 // The fan-out for games whose players move independently (G::kIndependentPlayers,
@@ -1292,10 +1452,11 @@ __global__ void __launch_bounds__(256) fanout_kernel(const FanParams p) {
 // session takes 16 + P - 1 lanes — 16 lanes for the speculated player in
 // branches 0-15, then one lane for every other player — instead of 16 x L, and
 // a wave holds 64 / (16 + P - 1) sessions (3 at P = 2..4: 89% of the lanes busy
-// at P = 4).  Cells and states go to column s * 32 + k (branch k of the
-// speculated player) or s * 32 + 16 + h (player h, one trajectory for all
-// branches) of planes Spad * 32 wide (the spec buffers hold Spad * 16 * L >=
-// Spad * 32 columns); try_select reads that layout.  Each branch cell's
+// at P = 4).  Cells and states go to column s * LS + k (branch k of the
+// speculated player) or s * LS + 16 + o (the o-th other player, one trajectory
+// for all branches), LS = 16 + P - 1 (indep_cols), of planes Spad * LS wide
+// (the spec buffers hold Spad * 16 * L >= Spad * LS columns); try_select reads
+// that layout.  Each branch cell's
 // checksum is assembled from the branch lane's part and the other players'
 // parts (lane shuffles within the session's lanes).
 template <class G>
@@ -1314,7 +1475,7 @@ __global__ void __launch_bounds__(256) fanout_indep_kernel(const FanParams p) {
   constexpr int L = G::kLanes;
   constexpr int P = G::kPlayers, IB = G::kInputBytes;
   constexpr int LS = indep_session_lanes<G>(), SPW = indep_sessions_per_wave<G>();
-  static_assert(IndepPlayers<G>::value && L > 1 && P <= kIndepLanes - kSpecBranches, "independent players, one per lane");
+  static_assert(IndepPlayers<G>::value && L > 1 && LS == indep_cols<G>(), "independent players, one per lane");
   const unsigned g = blockIdx.x * blockDim.x + threadIdx.x;
   const int wl = static_cast<int>(g % 64), j = wl / LS, r = wl % LS;
   if (j >= SPW) return;  // the wave's spare lanes
@@ -1322,7 +1483,7 @@ __global__ void __launch_bounds__(256) fanout_indep_kernel(const FanParams p) {
   if (s >= static_cast<unsigned>(p.S)) return;  // the session's lanes leave together
   const int lane0 = j * LS;                     // the session's first lane in the wave
   const unsigned Spad = static_cast<unsigned>(p.Spad), Gpad = Spad * L;
-  const unsigned Gs = Spad * kIndepLanes;  // spec plane width in this layout
+  const unsigned Gs = Spad * static_cast<unsigned>(LS);  // spec plane width in this layout
   const int W = p.W;
   const RingIO<IB> ring{const_cast<uint8_t*>(reinterpret_cast<const uint8_t*>(p.ring)), P, p.Spad};
   auto qrow = [&](int field, int h) { return p.qs[static_cast<size_t>(QS_PLAYER0 + field * 4 + h) * Spad + s]; };
@@ -1345,15 +1506,21 @@ __global__ void __launch_bounds__(256) fanout_indep_kernel(const FanParams p) {
   const int32_t base = la_rs + 1;
   const bool valid = p.status[s] != kP2PStatusPanic && !any_disc && rs >= 0 && base < cur && base + W > cur && base >= 0 &&
                      p.tag[static_cast<unsigned>(base % W) * Spad + s] == base;
+  uint32_t cand[4];  // the speculated player's candidates (every lane of the session computes the same)
+  fan_candidates(ring, max(rs, 0), s, la_rs, InputAlphabet<G>::value, p.fan_k, cand);
   if (r == 0) {
     p.spec_meta[SM_BASE * Spad + s] = base;
     p.spec_meta[SM_END * Spad + s] = cur;
     p.spec_meta[SM_PLAYER * Spad + s] = rs;
     p.spec_meta[SM_VALID * Spad + s] = valid ? 1 : 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) p.spec_meta[(SM_CAND + q) * Spad + s] = static_cast<int32_t>(cand[q]);
   }
   if (!valid) return;  // session-uniform
   const bool branch = r < kSpecBranches;
+  if (branch && r >= p.fan_k) return;  // no candidate for this branch lane
   const int k = branch ? r : 0;
+  const uint32_t ck = cand_at(cand, k);
   const int o = r - kSpecBranches;                        // the other players, in handle order, skipping rs
   const int h = branch ? rs : (o < rs ? o : o + 1);       // this lane's player
   uint32_t w[NW];
@@ -1361,7 +1528,10 @@ __global__ void __launch_bounds__(256) fanout_indep_kernel(const FanParams p) {
   const bool local = (p.local_mask >> h) & 1u;
   const int32_t la_h = qrow(QF_LAST_ADDED, h);
   const uint32_t pred = la_h == kNullFrame ? 0u : ring.get(la_h, h, s);
-  const unsigned col = s * kIndepLanes + static_cast<unsigned>(branch ? k : kSpecBranches + h);
+  uint32_t vin[kFanPre];
+  fan_prefetch(ring, h, s, base, cur, local, la_h, pred, vin);
+  const uint64_t vpk = fan_pack(vin);
+  const unsigned col = s * static_cast<unsigned>(LS) + static_cast<unsigned>(r);  // r = k, or 16 + the other-player index
   CS* __restrict__ cs = reinterpret_cast<CS*>(p.spec_cs);
   uint32_t frames = 0;
   for (int32_t f = base; f < cur; ++f) {
@@ -1378,14 +1548,16 @@ __global__ void __launch_bounds__(256) fanout_indep_kernel(const FanParams p) {
       if (branch) cs[(slot * Spad + s) * kSpecBranches + k] = G::fan_finish(Fl16{a.s1 + o1, a.s2 + o2}, f);
     }
     uint32_t v;
-    if (branch) v = static_cast<uint32_t>(k);
+    const int j = f - base;
+    if (branch) v = ck;
+    else if (j < kFanPre) v = fan_input(vpk, j);
     else if (local || (la_h != kNullFrame && f <= la_h)) v = ring.get(f, h, s);  // Confirmed
     else v = pred;  // repeat-last prediction (blank before the first input)
     advance_frame<G>(w, static_cast<InRec>(static_cast<uint64_t>(v) << (8 * IB * h)), h, 0u, &p.counters[1]);
     ++frames;
   }
   store_words<NW>(p.spec_state, static_cast<int>(Gs), static_cast<int>(col), w);
-  if (r == 0) p.stats[ST_BRANCH * Spad + s] += static_cast<unsigned long long>(frames) * kSpecBranches;
+  if (r == 0) p.stats[ST_BRANCH * Spad + s] += static_cast<unsigned long long>(frames) * p.fan_k;
 }
 
 }  // namespace rb

@@ -187,6 +187,7 @@ void rb_p2p_config_init(rb_p2p_config* c) {
   c->local_mask = 1u;     // handle 0 local, handle 1 remote (ex_game_p2p.rs's two-peer setup)
   c->remote_delay = 0;
   c->sparse_saving = 0;   // builder.rs:17 DEFAULT_SAVE_MODE
+  c->fanout_candidates = kSpecBranches;
 }
 
 const char* rb_p2p_last_error(const rb_p2p* b) { return b ? b->last_err.c_str() : g_p2p_err.c_str(); }
@@ -215,7 +216,10 @@ rb_status rb_p2p_create(const rb_p2p_config* cfg, rb_p2p** out) {
   if (!ops) return pfail(nullptr, RB_INVALID_REQUEST, "unsupported game / num_players combination");
   const bool fanout = (cfg->flags & RB_P2P_FLAG_FANOUT) != 0;
   if (fanout && (!ops->fanout_supported || cfg->sparse_saving))
-    return pfail(nullptr, RB_INVALID_REQUEST, "speculative fan-out needs ex_game with one lane per player, no sparse saving");
+    return pfail(nullptr, RB_INVALID_REQUEST,
+                 "speculative fan-out needs ex_game with one lane per player or the brawler, no sparse saving");
+  if (fanout && (cfg->fanout_candidates < 1 || cfg->fanout_candidates > kSpecBranches))
+    return pfail(nullptr, RB_INVALID_REQUEST, "fanout_candidates must be 1..16");
   if (static_cast<uint64_t>(cfg->max_prediction) * ops->nw * ops->lanes *
           ((static_cast<uint64_t>(cfg->num_sessions) + 63) / 64 * 64) >= (1ull << 32))
     return pfail(nullptr, RB_INVALID_REQUEST, "batch too large for 32-bit snapshot offsets");
@@ -390,6 +394,7 @@ rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs,
   p.sparse = b->cfg.sparse_saving != 0;
   p.sync_ticks = b->sync_ticks ? 1 : 0;
   p.fan_generic = b->fan_generic ? 1 : 0;
+  p.fan_k = b->cfg.fanout_candidates;
   p.spec_on = b->fanout ? 1 : 0;
   p.spec_state = b->spec_state;
   p.spec_cells = b->spec_cells;
@@ -414,6 +419,7 @@ rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs,
   fp.W = b->W;
   fp.local_mask = b->cfg.local_mask;
   fp.fan_generic = b->fan_generic ? 1 : 0;
+  fp.fan_k = b->cfg.fanout_candidates;
   P2P_TRY(b, hipSetDevice(b->device));
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (b->prof) {

@@ -41,6 +41,10 @@
 // same addresses in program order.
 #pragma once
 
+#ifndef RB_PIPE_FAST
+#define RB_PIPE_FAST 0  // 1: units run ExGame::advance_prepared_fast with the iteration redo (A/B builds)
+#endif
+
 namespace rb {
 
 template <class G, int CD>
@@ -187,19 +191,18 @@ __global__ void __launch_bounds__(256) steady_pipe_kernel(const RunParams p) {
       wB0[i] = B.w[i];
     }
     const int32_t mA0 = A.mismatch;
-    auto slots = [&](auto fast_tag) __attribute__((always_inline)) -> uint32_t {
+    // in_range_tag: B's rotations are all in [+0, 6.5) (prepare's in-range sincos); fast_tag: the
+    // branch-free AdvanceFrame (its flags are returned)
+    auto slots = [&](auto in_range_tag, auto fast_tag) __attribute__((always_inline)) -> uint32_t {
+      constexpr bool kInRange = decltype(in_range_tag)::value;
       constexpr bool kFast = decltype(fast_tag)::value;
       uint32_t special = 0;
       if constexpr (kB) {
         Dec decB[U];  // B's frames f0B .. f0B + CD
 #pragma unroll
         for (int k = 0; k < U; ++k) decB[k] = dec[k + 1];
-        if constexpr (kFast) {
-          special |= G::in_range(B.w) ? 0u : 1u;
-          G::template prepare<true, U>(B.w, decB, B.prep, nullptr);
-        } else {
-          G::template prepare<false, U>(B.w, decB, B.prep, &p.counters[1]);
-        }
+        if constexpr (kFast) special |= G::in_range(B.w) ? 0u : 1u;
+        G::template prepare<kInRange, U>(B.w, decB, B.prep, &p.counters[1]);
       }
 #pragma unroll
       for (int j = 0; j < H; ++j) {
@@ -209,7 +212,14 @@ __global__ void __launch_bounds__(256) steady_pipe_kernel(const RunParams p) {
       }
       return special;
     };
-    if (__any(slots(std::true_type{}) != 0u)) {
+    if constexpr (!RB_PIPE_FAST) {
+      // the general AdvanceFrame (branches around the rare paths), on the in-range sincos when
+      // B's whole wave starts in range (A's prep was chosen the same way one iteration earlier)
+      if (!kB || __all(G::in_range(B.w)))
+        slots(std::true_type{}, std::false_type{});
+      else
+        slots(std::false_type{}, std::false_type{});
+    } else if (__any(slots(std::true_type{}, std::true_type{}) != 0u)) {
       // a lane met an operand outside the fast form: the wave re-runs the iteration exactly
 #pragma unroll
       for (int i = 0; i < NW; ++i) {
@@ -218,7 +228,7 @@ __global__ void __launch_bounds__(256) steady_pipe_kernel(const RunParams p) {
       }
       A.mismatch = mA0;
       B.mismatch = kNullFrame;
-      slots(std::false_type{});
+      slots(std::false_type{}, std::false_type{});
     }
     if constexpr (kA) {
       const int32_t cA = A.f0 + CD;

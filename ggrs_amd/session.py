@@ -247,10 +247,13 @@ class SessionBuilder:
         self._sparse = bool(sparse_saving)
         return self
 
-    def with_speculative_fanout(self, on: bool) -> "SessionBuilder":
-        """P2P: presimulate 16 candidate inputs of the most-lagging remote handle
-        after every tick (RB_P2P_FLAG_FANOUT, BASELINE config 4)."""
+    def with_speculative_fanout(self, on: bool, candidates: int = 16) -> "SessionBuilder":
+        """P2P: presimulate `candidates` (1..16) candidate inputs of the
+        most-lagging remote handle after every tick (RB_P2P_FLAG_FANOUT,
+        BASELINE config 4): the whole input alphabet when it has at most that
+        many values (ex_game), else the most likely ones (include/ggrs_amd.h)."""
         self._fanout = bool(on)
+        self._fanout_k = int(candidates)
         return self
 
     def with_desync_detection_mode(self, interval: int) -> "SessionBuilder":  # builder.rs:169-172
@@ -299,6 +302,7 @@ class SessionBuilder:
             L.RB_P2P_FLAG_PEER_STATUS if getattr(self, "_peer_status", False) else 0)
         pc.block_size = self._cfg.block_size
         pc.desync_interval = getattr(self, "_desync", 0)
+        pc.fanout_candidates = getattr(self, "_fanout_k", 16)
         h = ctypes.c_void_p()
         st = lib.rb_p2p_create(ctypes.byref(pc), ctypes.byref(h))
         if st != L.RB_OK:

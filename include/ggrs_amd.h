@@ -242,16 +242,22 @@ typedef struct rb_p2p_config {
   uint32_t block_size;
   int32_t desync_interval; /* with_desync_detection_mode (builder.rs:167-172): DesyncDetection::On{interval}
                               for interval > 0, Off for 0 (the default, builder.rs:15) */
-  uint32_t reserved[3];
+  int32_t fanout_candidates; /* RB_P2P_FLAG_FANOUT: branches per session, 1..16 (default 16) */
+  uint32_t reserved[2];
 } rb_p2p_config;
 
 /* Speculative branch fan-out (BASELINE config 4): after every tick each session
- * presimulates 16 branches, one per candidate input (the 4-bit ex_game
- * alphabet) of the remote handle with the oldest unconfirmed input, over its
- * unconfirmed frames.  A later misprediction of that handle alone, held at
- * one value, becomes a branch select instead of LoadGameState + resimulation;
- * cells, states, statuses and frames stay identical to the plain rollback.
- * ex_game with one lane per player only; not with sparse saving. */
+ * presimulates K = fanout_candidates branches (at most 16), one per candidate
+ * input of the remote handle with the oldest unconfirmed input, over its
+ * unconfirmed frames.  The candidates are the game's whole input alphabet when
+ * it has at most K values (ex_game's 4 input bits, K = 16), else the K most
+ * likely values: the most recently confirmed distinct inputs of that handle,
+ * newest first (the reference's repeat-last prediction, input_queue.rs:126-140,
+ * is candidate 0), then the smallest values not taken.  A later misprediction
+ * of that handle alone, held at one candidate value, becomes a branch select
+ * instead of LoadGameState + resimulation; cells, states, statuses and frames
+ * stay identical to the plain rollback.  ex_game (one lane per player) and the
+ * brawler (one wave per session); not with sparse saving. */
 #define RB_P2P_FLAG_FANOUT 4u
 
 /* Peers' connect-status reports (update_player_disconnects, p2p_session.rs:707-742):

@@ -81,6 +81,8 @@ def load(path: str = LIB_PATH):
             "orc_bench_p2p_exgame": (ctypes.c_double, [I32, I32, I32, ctypes.c_uint32, I32, I32, I32, I32, I32, P,
                                                         P, P, I32, P, P]),
             "orc_wire_decode": (I32, [P, I32, P, I32, P, I32]),
+            "orc_bench_p2p_brawler": (ctypes.c_double, [I32, I32, I32, ctypes.c_uint32, I32, I32, I32, I32, I32, P,
+                                                         P, P, I32, P, P]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
@@ -383,7 +385,7 @@ def wire_decode(ref: bytes, data: bytes, cap: int = 4096):
 
 
 def bench_p2p_exgame(P: int, W: int, delay: int, local_mask: int, remote_delay: int, inputs, upto, remote_in,
-                     warmup: int, threads: int):
+                     warmup: int, threads: int, game: int = EX_GAME):
     """CPU 'port' baseline of the P2P rollback path on the given synthetic
     network arrays: (wall seconds of ticks [warmup, T), AdvanceFrames executed, errors)."""
     T, _, S = inputs.shape
@@ -392,6 +394,7 @@ def bench_p2p_exgame(P: int, W: int, delay: int, local_mask: int, remote_delay: 
     r = np.ascontiguousarray(remote_in, np.uint8)
     adv = np.zeros(1, np.int64)
     ne = np.zeros(1, np.int32)
-    t = load().orc_bench_p2p_exgame(P, W, delay, local_mask, remote_delay, S, T, warmup, threads, _ptr(a), _ptr(u),
-                                    _ptr(r), r.shape[0], _ptr(adv), _ptr(ne))
+    fn = load().orc_bench_p2p_brawler if game == BRAWLER else load().orc_bench_p2p_exgame
+    t = fn(P, W, delay, local_mask, remote_delay, S, T, warmup, threads, _ptr(a), _ptr(u), _ptr(r), r.shape[0],
+           _ptr(adv), _ptr(ne))
     return t, int(adv[0]), int(ne[0])

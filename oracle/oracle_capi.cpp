@@ -877,5 +877,11 @@ double orc_bench_p2p_exgame(int32_t P, int32_t W, int32_t delay, uint32_t local_
   return bench_p2p_game<exgame::Config, exgame::Game>(P, W, delay, local_mask, remote_delay, S, T, warmup, threads,
                                                       inputs, upto, remote_in, F, adv, n_err);
 }
+double orc_bench_p2p_brawler(int32_t P, int32_t W, int32_t delay, uint32_t local_mask, int32_t remote_delay, int32_t S,
+                             int32_t T, int32_t warmup, int32_t threads, const uint8_t* inputs, const int32_t* upto,
+                             const uint8_t* remote_in, int32_t F, int64_t* adv, int32_t* n_err) {
+  return bench_p2p_game<brawler::Config, brawler::Game>(P, W, delay, local_mask, remote_delay, S, T, warmup, threads,
+                                                        inputs, upto, remote_in, F, adv, n_err);
+}
 }  // extern "C"
 

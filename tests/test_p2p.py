@@ -194,10 +194,10 @@ def test_oracle_disconnect_resimulates_to_the_disconnected_truth(game, sparse):
 
 
 # ---------------------------------------------------------------------------- device vs oracle
-def gpu_pair(game, S, P, W, d, rd, mask, sparse, lane_per_session=False, fanout=False):
+def gpu_pair(game, S, P, W, d, rd, mask, sparse, lane_per_session=False, fanout=False, candidates=16):
     b = (G.SessionBuilder(game, num_sessions=S).with_num_players(P).with_max_prediction_window(W)
          .with_input_delay(d).with_sparse_saving_mode(sparse).with_remote_input_delay(rd)
-         .with_lane_per_session(lane_per_session).with_speculative_fanout(fanout))
+         .with_lane_per_session(lane_per_session).with_speculative_fanout(fanout, candidates))
     for h in range(P):
         b.add_player(PlayerType.Local if (mask >> h) & 1 else PlayerType.Remote, h)
     sess = b.start_p2p_session()
@@ -308,17 +308,22 @@ def test_gpu_p2p_fused_launch_equals_per_tick(gpu_available):
         np.testing.assert_array_equal(x, y)
 
 
-FUSED_CASES = [  # game, P, W, d, rd, local_mask, lag range, ticks per launch
-    (G.Game.EX_GAME, 2, 8, 2, 2, 0b01, (0, 6), 16),
-    (G.Game.EX_GAME, 4, 8, 1, 1, 0b0001, (1, 5), 24),
-    (G.Game.EX_GAME, 3, 7, 0, 2, 0b010, (0, 4), 32),
-    (G.Game.EX_GAME, 2, 4, 0, 0, 0b01, (1, 6), 12),  # PredictionThreshold ticks inside the launches
+FUSED_CASES = [  # game, P, W, d, rd, local_mask, lag range, ticks per launch, sparse saving
+    (G.Game.EX_GAME, 2, 8, 2, 2, 0b01, (0, 6), 16, False),
+    (G.Game.EX_GAME, 4, 8, 1, 1, 0b0001, (1, 5), 24, False),
+    (G.Game.EX_GAME, 3, 7, 0, 2, 0b010, (0, 4), 32, False),
+    (G.Game.EX_GAME, 2, 4, 0, 0, 0b01, (1, 6), 12, False),  # PredictionThreshold ticks inside the launches
+    # sparse saving on the lane-asynchronous kernel (launches of >= 24 ticks): check_last_saved_state's
+    # second rollback inside the launch, PredictionThreshold from the dry run
+    (G.Game.EX_GAME, 2, 8, 2, 1, 0b10, (1, 5), 32, True),
+    (G.Game.EX_GAME, 3, 7, 0, 2, 0b010, (0, 4), 48, True),
+    (G.Game.EX_GAME, 2, 4, 0, 0, 0b01, (1, 6), 24, True),
 ]
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("sync_ticks", [False, True], ids=["async", "lockstep"])
-@pytest.mark.parametrize("case", FUSED_CASES, ids=[f"P{c[1]}-W{c[2]}-d{c[3]}-rd{c[4]}-m{c[5]}-tpl{c[7]}"
+@pytest.mark.parametrize("case", FUSED_CASES, ids=[f"P{c[1]}-W{c[2]}-d{c[3]}-rd{c[4]}-m{c[5]}-tpl{c[7]}-sp{int(c[8])}"
                                                    for c in FUSED_CASES])
 def test_gpu_p2p_fused_launches_match_oracle(gpu_available, monkeypatch, case, sync_ticks):
     # Multi-tick launches with sessions of different lags, so that inside a launch
@@ -328,11 +333,11 @@ def test_gpu_p2p_fused_launches_match_oracle(gpu_available, monkeypatch, case, s
     # the oracle's.
     import torch
     monkeypatch.setenv("RB_P2P_SYNC_TICKS", "1" if sync_ticks else "0")
-    game, P, W, d, rd, mask, (lo, hi), tpl = case
+    game, P, W, d, rd, mask, (lo, hi), tpl, sparse = case
     S, T = 300, 96
     inputs, upto, rin = synth_network(S, P, T, mask, rd, lo, hi)
     di, du, dr = (torch.from_numpy(a).cuda() for a in (inputs, upto, rin))
-    sess, orc = gpu_pair(game, S, P, W, d, rd, mask, False)
+    sess, orc = gpu_pair(game, S, P, W, d, rd, mask, sparse)
     for t0 in range(0, T, tpl):
         t1 = min(T, t0 + tpl)
         sess.run_ticks(di[t0:t1], du[t0:t1], dr)
@@ -387,6 +392,43 @@ def test_gpu_speculative_fanout_matches_rollback(gpu_available, monkeypatch, cas
     assert branch_frames > 0
     # no panic, and no lane (the padding lane of P = 3 included) ever took the
     # out-of-range math path: a selected branch never hands a lane garbage
+    assert sess.counters()[2] == 0 and sess.counters()[1] == 0
+
+
+FANOUT_K_CASES = [  # game, P, W, d, rd, local_mask, lag, K, input mask
+    (G.Game.EX_GAME, 4, 8, 1, 1, 0b0001, (1, 5), 6, 0x0F),   # K < the 16-value alphabet: the most likely 6
+    (G.Game.EX_GAME, 2, 8, 2, 2, 0b01, (0, 6), 2, 0x0F),     # K = 2: the prediction and the input before it
+    (G.Game.BRAWLER, 2, 8, 1, 1, 0b01, (1, 5), 16, 0x07),    # the brawler: a wave per branch, 8-bit inputs
+    (G.Game.BRAWLER, 3, 6, 0, 1, 0b010, (1, 4), 8, 0x1F),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", FANOUT_K_CASES, ids=[f"{c[0].name}-P{c[1]}-K{c[7]}-m{c[8]:x}" for c in FANOUT_K_CASES])
+def test_gpu_fanout_top_k_candidates_match_rollback(gpu_available, case):
+    # The fan-out with K most-likely candidates (include/ggrs_amd.h RB_P2P_FLAG_FANOUT): every
+    # select must stay observably identical to the reference's rollback (the oracle) on every tick,
+    # for ex_game with K below its alphabet and for the brawler (one wave per branch, 8-bit inputs,
+    # candidates = the most recently confirmed distinct inputs).
+    import torch
+    game, P, W, d, rd, mask, (lo, hi), K, imask = case
+    S, T = (48, 60) if game == G.Game.BRAWLER else (96, 80)
+    inputs, upto, rin = synth_network(S, P, T, mask, rd, lo, hi, mask=imask)
+    sess, orc = gpu_pair(game, S, P, W, d, rd, mask, False, fanout=True, candidates=K)
+    di, du, dr = (torch.from_numpy(a).cuda() for a in (inputs, upto, rin))
+    for t in range(T):
+        sess.run_ticks(di[t:t + 1], du[t:t + 1], dr)
+        ost, olf, ona, ons = drive_oracle(orc, mask, inputs, upto, rin, t + 1, t0=t)[0]
+        st, lf, na, ns = sess.status()
+        np.testing.assert_array_equal(st, ost, err_msg=f"status, tick {t}")
+        np.testing.assert_array_equal(lf, olf, err_msg=f"rollback frame, tick {t}")
+        np.testing.assert_array_equal(na, ona, err_msg=f"AdvanceFrame count, tick {t}")
+        np.testing.assert_array_equal(ns, ons, err_msg=f"SaveGameState count, tick {t}")
+        if t % 10 == 9 or t == T - 1:
+            compare_state(sess, orc, t)
+    adv, saves, loads, selects, branch_frames = sess.totals()
+    assert selects > 0, "no misprediction was served by a branch select"
+    assert branch_frames > 0
     assert sess.counters()[2] == 0 and sess.counters()[1] == 0
 
 

@@ -6,6 +6,8 @@
 // (inline asm, so nothing is folded) and stamps s_memtime around the loop;
 // the program prints cycles per instruction per wave and per SIMD
 // (= per-wave cycles / waves per SIMD).  C = 8: issue cost; C = 1: latency.
+// OP 7 (v_cndmask with a vcc clobber) is inflated by the s_nop 0 the compiler puts
+// before each instance (the clobber reads as a VALU write of vcc): use OP 19-20.
 // Build: hipcc -O3 --offload-arch=gfx950 -o tools/build/ubench_valu tools/ubench_valu.hip
 #include <hip/hip_runtime.h>
 
@@ -45,12 +47,22 @@ __device__ __forceinline__ void op1(float& f, double& d, uint32_t& u, uint64_t& 
   if constexpr (OP == 16) asm volatile("v_cmp_gt_f32 vcc, %0, %1" ::"v"(f), "v"(a) : "vcc");
   if constexpr (OP == 17) asm volatile("v_div_fmas_f32 %0, %0, %1, %1" : "+v"(f) : "v"(a) : "vcc");
   if constexpr (OP == 18) asm volatile("v_cvt_f64_i32 %0, %1" : "=v"(d) : "v"(u));
+  // selects without the vcc clobber of OP 7 (which makes the compiler put an s_nop before each one):
+  // a loop-invariant SGPR-pair mask, a cmp + select pair as the kernels emit it, and a bit select
+  if constexpr (OP == 19) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(u) : "v"(ua), "s"(static_cast<uint64_t>(ua) * 0x9E3779B97F4A7C15ull));
+  if constexpr (OP == 20) asm volatile("v_cmp_gt_u32_e64 s[40:41], %0, %1\n\ts_nop 1\n\tv_cndmask_b32_e64 %0, %0, %1, s[40:41]" : "+v"(u) : "v"(ua) : "s40", "s41");
+  if constexpr (OP == 21) asm volatile("v_bfi_b32 %0, %1, %0, %2" : "+v"(u) : "v"(ua), "v"(ua));
+  if constexpr (OP == 22) asm volatile("s_nop 0" : "+v"(u));
+  if constexpr (OP == 23) asm volatile("v_med3_f32 %0, %0, %1, %2" : "+v"(f) : "v"(a), "v"(a));
+  if constexpr (OP == 24) asm volatile("v_max_f32 %0, %0, %1" : "+v"(f) : "v"(a));
 }
 static const char* kNames[] = {"v_fma_f32",     "v_fma_f64",      "v_mul_f64",     "v_cvt_f32_f64",  "v_cvt_f64_f32",
                                "v_cvt_i32_f64", "v_dot4_u32_u8",  "v_cndmask_b32", "v_sqrt_f32",     "v_rcp_f32",
                                "v_pk_fma_f32",  "v_add_u32",      "v_mul_hi_u32",  "v_lshl_add_u64", "v_add_u32_dpp",
-                               "v_add_f64",     "v_cmp_gt_f32",   "v_div_fmas_f32", "v_cvt_f64_i32"};
-constexpr int kOps = 19;
+                               "v_add_f64",     "v_cmp_gt_f32",   "v_div_fmas_f32", "v_cvt_f64_i32",
+                               "cndmask_sgpr",  "cmp+nop1+cndmask", "v_bfi_b32",    "s_nop 0",        "v_med3_f32",
+                               "v_max_f32"};
+constexpr int kOps = 25;
 
 template <int OP, int C>
 __global__ void __launch_bounds__(256) ubench(uint64_t* out, float seed) {
