@@ -667,12 +667,18 @@ rb_status rb_p2p_profile_enable(rb_p2p* b, int32_t on) {
   // the event pool is created here, outside any timed region
   if (b->prof) {
     P2P_TRY(b, hipSetDevice(b->device));
+    const size_t fresh = b->prof_ev.size();
     while (b->prof_ev.size() < 256) {
       hipEvent_t e0 = nullptr, e1 = nullptr;
       P2P_TRY(b, hipEventCreate(&e0));
       P2P_TRY(b, hipEventCreate(&e1));
       b->prof_ev.emplace_back(e0, e1);
     }
+    for (size_t i = fresh; i < b->prof_ev.size(); ++i) {  // first records (signal set-up) outside timed regions
+      P2P_TRY(b, hipEventRecord(b->prof_ev[i].first, b->stream));
+      P2P_TRY(b, hipEventRecord(b->prof_ev[i].second, b->stream));
+    }
+    P2P_TRY(b, hipStreamSynchronize(b->stream));
   }
   return RB_OK;
 }

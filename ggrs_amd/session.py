@@ -494,6 +494,38 @@ class SyncTestSession(_StreamOrdered):
         _raise(self._lib, self._h, st)
         return done.value
 
+    def prepare_ticks(self, inputs):
+        """run_ticks(inputs) as a prepared native call, for a host loop whose
+        per-call cost matters (a compiled host calls rb_run_ticks directly):
+        the pointer, stride and status slot are built here, once, and the
+        returned ``call()`` is the bare C call.  ``call()`` returns the
+        rb_status and ``check(status)`` turns it into run_ticks' return value
+        or exception.  ``inputs`` must be a CUDA tensor [T, num_players,
+        num_sessions] that outlives the calls, and they must be made with
+        torch's current stream equal to the batch stream (set_stream), so
+        that stream order alone orders them against torch's work."""
+        T = int(inputs.shape[0])
+        per_tick = self._num_players * self.num_sessions
+        ptr, dev, _ = self._as_input(inputs, T * per_tick)
+        if not dev or T <= 0:
+            raise InvalidRequest("prepare_ticks takes a non-empty CUDA tensor")
+        if self._pre() is not None:
+            raise InvalidRequest("prepare_ticks: torch's current stream must be the batch stream (set_stream)")
+        done = ctypes.c_int32()
+        fn, args = self._lib.rb_run_ticks, (self._h, T, ptr, per_tick * np.dtype(self.input_dtype).itemsize, 1,
+                                            ctypes.byref(done))
+
+        def call():
+            return fn(*args)
+
+        def check(st):
+            if st == L.RB_MISMATCHED_CHECKSUM:
+                raise MismatchedChecksum(self.mismatches())
+            _raise(self._lib, self._h, st)
+            return done.value
+
+        return call, check
+
     # -- batch extras
     def last_requests(self) -> "RequestList":
         cap = 4 * self._max_prediction + 8

@@ -481,3 +481,35 @@ def test_run_ticks_fused_mismatch_and_corruption(gpu_available, monkeypatch, pip
     assert list(np.nonzero(ei.value.frames != -1)[0]) == [5, 33]
     compare_live(sess, orc, G.Game.EX_GAME)
     compare_cells(sess, orc, P, G.Game.EX_GAME)  # frozen sessions' cells end as after their failing tick
+
+
+def test_prepared_ticks_same_as_run_ticks(gpu_available):
+    """session.prepare_ticks (bench.py's timed loop: the native call built
+    ahead) runs exactly run_ticks: chunks of ticks through prepared calls on
+    the batch stream, bit-exact with the oracle; an error status raises like
+    run_ticks."""
+    import torch
+    S, P, cd, d, T = 130, 2, 7, 2, 70
+    inputs = synth_inputs(S, P, T, seed=91)
+    sess, orc = make_pair(G.Game.EX_GAME, S, P, 8, cd, d)
+    stream = torch.cuda.Stream()
+    sess.set_stream(stream)
+    dev = torch.from_numpy(inputs).cuda()
+    t = 0
+    with torch.cuda.stream(stream):
+        for n in (8, 5, 20, 1, 36):
+            call, check = sess.prepare_ticks(dev[t:t + n])
+            assert check(call()) == n
+            for k in range(t, t + n):
+                for h in range(P):
+                    orc.add_local_input(h, inputs[k, h])
+                kinds, _ = orc.advance()
+                assert (kinds == 0).all()
+            t += n
+        assert [(int(r.kind), r.frame) for r in sess.last_requests()] == orc.trace(0)
+        compare_cells(sess, orc, P, G.Game.EX_GAME)
+        compare_live(sess, orc, G.Game.EX_GAME)
+        with pytest.raises(G.InvalidRequest):
+            sess.prepare_ticks(dev[0:0])
+    with pytest.raises(G.InvalidRequest):  # torch's current stream is not the batch stream
+        sess.prepare_ticks(dev[0:1])
