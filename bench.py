@@ -424,14 +424,12 @@ def bench_p2p(args):
             # and its inputs; per session-tick the base cell load and K branch states stored; per select the
             # selected cells read back
             bytes_rank += branch / world * (state + 2 + P) + S * args.steps * state * (K + 1) + selects / world * state
-        elif args.fanout:  # fanout_indep_kernel: the players not speculated on are simulated once per
-            # session, so per presimulated frame 16 x (the speculated player's cell part + checksum + input)
-            # + (P - 1) x (a player's cell part + input); per session-tick the base cell load and the final
-            # states (16 speculated + P - 1 others); per select the selected cells read back
+        elif args.fanout:  # the in-kernel fan-out (p2p.hpp inlane_fan): only the speculated player's words
+            # are branched, so per presimulated branch frame its part of the cell (state / P) is stored (the
+            # base frame's excepted: one per branch per session-tick), per session-tick the K final branch
+            # parts; per select the selected branch's parts read back (its frames: about the branch depth)
             ps = state // P
-            frames = branch / world / K
-            bytes_rank += (frames * (K * (ps + 2 + 1) + (P - 1) * (ps + 1)) + S * args.steps * (state + (K + P - 1) * ps)
-                           + selects / world * state)
+            bytes_rank += branch / world * ps + S * args.steps * K * ps + selects / world * ps * 2
         avg_kernel_s = kernel_ms / 1e3 / max(1, launches)
         cfg_key = (f"p2p {args.game} P={P} W={W} d={args.input_delay} rd={args.remote_delay} lag={lo},{hi} S={S}"
                    + (" sparse" if args.sparse_saving else "") + (f" fanout{'' if K == 16 else K}" if args.fanout else "")
@@ -439,7 +437,7 @@ def bench_p2p(args):
         gname = f"Brawler<{P}>" if brawler else f"ExGame<{P},true>"
         roofline = roofline_block(bytes_rank / max(1, launches), avg_kernel_s, args.steps / max(1, launches), launches,
                                   f"p2p_kernel<{gname}>" + ((" + fanout_kernel (per tick)" if generic_fan or brawler
-                                                             else " + fanout_indep_kernel (per tick)")
+                                                             else " with the in-kernel fan-out (fused P2P ticks)")
                                                             if args.fanout
                                                             else " (fused P2P ticks)"),
                                   pmc_profile(cfg_key), "algorithmic: cells loaded/saved, inputs, deliveries")

@@ -425,12 +425,12 @@ struct ExGame {
     return fl16_finish(a);
   }
 
-  // ---- independent players (the speculative fan-out, p2p.hpp
-  // fanout_indep_kernel): State::advance (:259-321) moves every player from its
-  // own input alone, so the players the fan-out does not speculate on follow
-  // one trajectory in all 16 branches and are simulated once per session.
-  // The checksum of a branch cell is then assembled from per-player parts:
-  // fan_partial of each player's words, summed, and fan_finish.
+  // ---- independent players (the in-kernel speculative fan-out, p2p.hpp
+  // inlane_fan): State::advance (:259-321) moves every player from its own
+  // input alone, so the branches of the speculated player are simulated on
+  // that player's words alone and the other players keep the main
+  // trajectory's.  The checksum of a branch cell is then assembled from
+  // per-player parts: fan_partial of each player's words, summed, and fan_finish.
   static constexpr bool kIndependentPlayers = kSplit;
   __device__ static Fl16 fan_partial(const uint32_t (&w)[NWL], int i) {  // player i's words (one player per lane)
     Fl16 a{0u, 0u};

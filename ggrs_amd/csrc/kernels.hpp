@@ -680,6 +680,7 @@ struct GameOps {
   virtual hipError_t launch_p2p(const P2PParams& p, int block, hipStream_t st) const = 0;
   virtual hipError_t launch_fanout(const FanParams& p, int block, hipStream_t st) const = 0;
   bool fanout_supported = false;
+  bool inlane_fanout = false;  // p2p_kernel runs the fan-out itself (inlane_fan), unless fan_generic
 };
 
 template <class G>
@@ -695,6 +696,7 @@ struct GameOpsT final : GameOps {
     image_bytes = G::kImageBytes;
     display = G::kDisplay;
     fanout_supported = kFanout;
+    inlane_fanout = kFanout && inlane_fan<G>();
   }
   void word_loc(int k, int* lane, int* word) const override { G::word_loc(k, lane, word); }
   void init_words(uint32_t* w) const override { G::init(w); }
@@ -753,13 +755,15 @@ struct GameOpsT final : GameOps {
   template <bool kSpec, bool kSparse, bool kNet>
   static hipError_t launch_p2p_as(const P2PParams& p, int grid, int block, hipStream_t st) {
     size_t lds = p2p_lds_bytes<G>(block);
-    if constexpr (!kSpec && !kNet && p2p_lds_queue<G>()) {
+    if constexpr ((!kSpec || inlane_fan<G>()) && !kNet && p2p_lds_queue<G>()) {
       // the snapshot ring in LDS (p2p_lds_cell_bytes) for launches of many ticks: it is copied in and
-      // written back whole, which short launches (the wire path's one tick per launch) do not repay
-      if (p2p_lds_cells<G>(p.W, block) && p.T >= kLdsCellsMinTicks) {
-        // lane-asynchronous ticks (plain path and sparse saving) unless the batch asked for lock-step ticks
-        auto k = !p.sync_ticks ? p2p_kernel<G, kSpec, kSparse, kNet, true, true>
-                               : p2p_kernel<G, kSpec, kSparse, kNet, true, false>;
+      // written back whole, which short launches (the wire path's one tick per launch) do not repay;
+      // with the fan-out only for the in-kernel one (fanout_kernel reads the HBM cells between ticks)
+      if (p2p_lds_cells<G>(p.W, block) && p.T >= kLdsCellsMinTicks && (!kSpec || !p.fan_generic)) {
+        // lane-asynchronous ticks (plain path and sparse saving) unless the batch asked for lock-step
+        // ticks; the fan-out runs lock-step ticks
+        auto k = (!p.sync_ticks && !kSpec) ? p2p_kernel<G, kSpec, kSparse, kNet, true, !kSpec>
+                                           : p2p_kernel<G, kSpec, kSparse, kNet, true, false>;
         lds += p2p_lds_cell_bytes<G>(block, p.W);
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                            static_cast<int>(lds));
@@ -787,14 +791,6 @@ struct GameOpsT final : GameOps {
   // fan-out: one lane per player (ex_game) or one wave per session (the brawler), 1-byte inputs
   static constexpr bool kFanout = ((G::kLanes > 1 && G::kLanes <= 4) || G::kLanes == 64) && G::kInputBytes == 1;
   hipError_t launch_fanout(const FanParams& p, int block, hipStream_t st) const override {
-    if constexpr (kFanout && IndepPlayers<G>::value) {  // the players the fan-out does not speculate on, once
-      if (!p.fan_generic) {
-        const int waves = (p.S + indep_sessions_per_wave<G>() - 1) / indep_sessions_per_wave<G>();
-        const int grid = (waves * 64 + block - 1) / block;
-        hipLaunchKernelGGL(fanout_indep_kernel<G>, dim3(grid), dim3(block), 0, st, p);
-        return hipGetLastError();
-      }
-    }
     if constexpr (kFanout) {
       const int grid = (p.Spad * kSpecBranches * G::kLanes + block - 1) / block;
       hipLaunchKernelGGL(fanout_kernel<G>, dim3(grid), dim3(block), 0, st, p);

@@ -240,15 +240,18 @@ struct P2PParams {
   // per-session work counters [ST_COUNT][Spad] (no same-address atomics: each
   // session's lead lane owns its column; the host sums on demand)
   unsigned long long* stats;
-  // speculative fan-out (fanout_kernel below; spec_on = 0: plain P2P)
-  // branch-major columns: column (s * kSpecBranches + k) * L + lane, so one
-  // session's 16 branches x L lanes store 64 consecutive words per plane
-  const uint32_t* spec_state;  // [NW planes][Spad*16*L] branch states at meta end
-  const uint32_t* spec_cells;  // [W][NW planes][Spad*16*L] branch cells
-  const void* spec_cs;         // [W][Spad][16] CS
-  const int32_t* spec_meta;    // [SM_COUNT][Spad]
+  // speculative fan-out (spec_on = 0: plain P2P).  fanout_kernel (below, a
+  // launch of its own between one-tick P2P launches): branch-major columns
+  // (s * kSpecBranches + k) * L + lane, so one session's 16 branches x L lanes
+  // store 64 consecutive words per plane.  The in-kernel fan-out (kInFan):
+  // column s * kSpecBranches + k of planes Spad * 16 wide, the speculated
+  // player's words only.
+  uint32_t* spec_state;  // [NW planes][Spad*16*L] branch states at meta end
+  uint32_t* spec_cells;  // [W][NW planes][Spad*16*L] branch cells
+  const void* spec_cs;   // [W][Spad][16] CS (fanout_kernel)
+  int32_t* spec_meta;    // [SM_COUNT][Spad]
   int32_t spec_on;
-  int32_t fan_generic;  // the branches were left by fanout_kernel, not fanout_indep_kernel
+  int32_t fan_generic;  // the branches come from fanout_kernel (RB_FANOUT_GENERIC=1, or a game without kInFan)
   int32_t fan_k;        // candidates (branches) per session, <= kSpecBranches
   const uint8_t* local_in;  // tick t, handle h: local_in + t * local_stride + (h * S + s) * IB
   int64_t local_stride;
@@ -542,19 +545,29 @@ __device__ __forceinline__ uint32_t q_input(DevQueue& q, const R& r, int h, unsi
   return q.pred_val;  // Predicted
 }
 
-// The speculative fan-out runs fanout_indep_kernel for games whose players move
-// independently, unless the batch asks for the generic fanout_kernel
-// (fan_generic: RB_FANOUT_GENERIC=1 at create, for A/B and tests).
-// fanout_indep_kernel's spec columns per session: the 16 branches of the
-// speculated player, then the P - 1 other players (handle order, skipping the
-// speculated one), with no padding between sessions: every 128-byte line of a
-// spec plane is written whole (a 32-column block per session left 13 of 32
-// columns unwritten at P = 4 and its partial lines cost 1.6x the algorithmic
-// store bytes, round 2's C4 profile)
+// The in-kernel fan-out (p2p_kernel kSpec, kInFan).  For a game whose players
+// move independently (G::kIndependentPlayers: every player's state follows from
+// its own inputs alone, ex_game.rs:259-321) and that reads no input status, the
+// 16 branches of a session differ only in the speculated player's words, and
+// the other players' words in every branch are those of the main trajectory:
+// a select (try_select) is only taken when no other player mispredicted, so
+// their cells and states are already what the rollback would compute.  So the
+// fan-out simulates the speculated player alone, 16 / L branches in each of
+// the session's L lanes (independent chains: ILP), at the end of every tick
+// inside p2p_kernel itself; the spec columns are per branch (column
+// s * 16 + k, branch k = b * L + lane is owned by lane k % L, which alone
+// writes and reads it back: same thread, program order).  A select takes the
+// branch's words for the speculated player's column and rebuilds each cell's
+// checksum from per-player fletcher parts (the branch's part and the other
+// players' parts of their own cell words).  The fan-out running in the tick
+// lets a launch hold many ticks (the two-launch fan-out needed one P2P launch
+// per tick: every lane of a session's branches ran between ticks).
 template <class G>
-constexpr int indep_cols() {
-  return kSpecBranches + G::kPlayers - 1;
+constexpr bool inlane_fan() {
+  if constexpr (IndepPlayers<G>::value) return G::kLanes > 1 && G::kLanes <= 4 && !G::kUsesStatus && G::kInputBytes == 1;
+  else return false;
 }
+constexpr int kFanGroup = 4;  // branches a lane advances together (its independent chains)
 
 // kSpec / kSparse / kNet: the fan-out select, sparse saving and the
 // network-fed bookkeeping (desync detection, peers' connect-status reports)
@@ -611,8 +624,11 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     if constexpr (kLdsQ) return LdsRing{lds_queue + threadIdx.x, blockDim.x};
     else return hbm;
   }();
-  static_assert(!kLdsC || (kLdsQ && !kSpec && !kNet),
-                "the LDS snapshot ring needs the LDS queue; the fan-out and desync detection read HBM cells mid-launch");
+  // the in-kernel fan-out (the batch's branches are this kernel's own unless fan_generic)
+  constexpr bool kInFan = kSpec && inlane_fan<G>();
+  const bool in_fan = kInFan && !p.fan_generic;
+  static_assert(!kLdsC || (kLdsQ && (!kSpec || kInFan) && !kNet),
+                "the LDS snapshot ring needs the LDS queue; fanout_kernel and desync detection read HBM cells mid-launch");
   const unsigned bd = blockDim.x, tid = threadIdx.x, sl = tid / L, bps = bd / L;
   uint32_t* const lds_cell = reinterpret_cast<uint32_t*>(lds_queue + kQueueLen * bd);  // [W][NW][bd]
   int32_t* const lds_tag = reinterpret_cast<int32_t*>(lds_cell + static_cast<unsigned>(W) * NW * bd);  // [W][bps]
@@ -671,12 +687,15 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
   // LDS queue: the HBM frames this launch can read.  Reads are of frames
   // >= cur - W (adjust_gamestate checks that before it advances) up to the
   // last added one, or of the last added frame itself (predictions and the
-  // delay replication); every later frame is added inside the launch.
+  // delay replication); every later frame is added inside the launch.  The
+  // in-kernel fan-out choosing K of a larger alphabet also reads the 32 frames
+  // up to the last added one (fan_candidates).
   const int32_t la0 = q[0].last_added;
   if constexpr (kLdsQ) {
     const int h = player_of(0);
+    const int32_t back = (in_fan && InputAlphabet<G>::value > static_cast<uint32_t>(p.fan_k)) ? 32 : 0;
     if (h < P && la0 != kNullFrame) {
-      const int32_t lo = max(max(0, la0 - (kQueueLen - 1)), min(cur - W, la0));
+      const int32_t lo = max(max(0, la0 - (kQueueLen - 1)), min(cur - W, la0) - back);
       for (int32_t f0 = lo; f0 <= la0; f0 += 8) {  // 8 loads in flight per round trip
         uint32_t v[8];
 #pragma unroll
@@ -824,6 +843,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
   // predictions for the others, confirmed local inputs).  The sync layer's
   // bookkeeping runs as in adjust (dry), the cells and the state are copied.
   auto try_select = [&](int32_t first_incorrect, int32_t min_confirmed) __attribute__((always_inline)) -> bool {
+    if (kLdsC && !in_fan) return false;  // (not launched: fanout_kernel's branches need HBM cells)
     if (any_disc || disc_frame != kNullFrame) return false;  // the branches assumed everybody connected
     if (!sm_valid || sm_end != cur) return false;
     const int32_t base = sm_base;
@@ -854,34 +874,82 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     adjust(first_incorrect, min_confirmed);
     exec = true;
     if (status == kP2PStatusPanic) return true;
-    // branch kk, this lane: column (s * 16 + kk) * L + lane of planes Spad * 16 * L wide; with independent
-    // players (fanout_indep_kernel) column s * 32 + kk of the speculated player's lane, s * 32 + 16 + lane
-    // of any other player's (one trajectory for all branches), planes Spad * 32 wide
-    const bool indep = IndepPlayers<G>::value && !p.fan_generic;
-    constexpr unsigned LS = static_cast<unsigned>(indep_cols<G>());
-    const unsigned Gs = indep ? Spad * LS : Gpad * kSpecBranches;
-    const unsigned col = !indep ? (s * kSpecBranches + static_cast<unsigned>(kk)) * L + lane
-                                : s * LS + (lane == rs ? static_cast<unsigned>(kk)
-                                                       : kSpecBranches + static_cast<unsigned>(lane < rs ? lane : lane - 1));
-    const CS* __restrict__ scs = reinterpret_cast<const CS*>(p.spec_cs);
-    // the padding lane of a 4-lane group (P = 3, one lane per player) holds no player: no branch
-    // column was written for it (fanout_indep_kernel), so it keeps its own words; nothing observes
-    // them.  (A wave-per-session game holds state in every lane.)
-    const bool real = !kSplit || L == 64 || lane < P;
-    for (int32_t f = base + 1; f < cur; ++f) {  // the cells adjust would have saved
-      const unsigned slot = static_cast<unsigned>(f % W);
-      if (real) {
+    if (in_fan) {
+      // the in-kernel fan-out's branch kk: column s * 16 + kk, written by lane kk % L (which alone reads
+      // it back and hands the words to the speculated player's lane); every other lane keeps its own
+      // cells and state (no misprediction of its player), and each cell's checksum is rebuilt from the
+      // players' fletcher parts
+      if constexpr (kInFan) {
+        const unsigned Gs = Spad * static_cast<unsigned>(kSpecBranches + L);
+        const int owner = kk % L;
+        const unsigned col = s * kSpecBranches + static_cast<unsigned>(kk);
+        const unsigned ocol = Spad * kSpecBranches + s * L + static_cast<unsigned>(lane);  // this lane's player, once
+        const bool other = lane < P && lane != rs;
+        const int src = static_cast<int>(__lane_id()) - lane + owner;
+        for (int32_t f = base + 1; f < cur; ++f) {  // the cells adjust would have saved
+          const unsigned slot = static_cast<unsigned>(f % W);
+          uint32_t bw[NW], cw[NW] = {};
+          if (lane == owner) load_words<NW>(p.spec_cells + slot * NW * Gs, static_cast<int>(Gs), static_cast<int>(col), bw);
+#pragma unroll
+          for (int n = 0; n < NW; ++n) bw[n] = static_cast<uint32_t>(__shfl(static_cast<int>(bw[n]), src, 64));
+          if (other) load_words<NW>(p.spec_cells + slot * NW * Gs, static_cast<int>(Gs), static_cast<int>(ocol), cw);
+          if (lane == rs || other) {
+            if (lane == rs) {
+#pragma unroll
+              for (int n = 0; n < NW; ++n) cw[n] = bw[n];
+            }
+            if constexpr (kLdsC) {
+#pragma unroll
+              for (int n = 0; n < NW; ++n) lds_cell[(slot * NW + n) * bd + tid] = cw[n];
+            } else {
+              store_words<NW>(p.snap + slot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), cw);
+            }
+          }
+          Fl16 a{0u, 0u};
+          if (lane < P) a = G::fan_partial(cw, lane);  // (the padding lane of P = 3 holds no player)
+          a.s1 = group_sum<L>(a.s1);
+          a.s2 = group_sum<L>(a.s2);
+          const CS c = G::fan_finish(a, f);
+          if (lead) {
+            if constexpr (kLdsC) {
+              lds_cs[slot * bps + sl] = c;
+              lds_tag[slot * bps + sl] = f;
+            } else {
+              csa[slot * Spad + s] = c;
+              p.tag[slot * Spad + s] = f;
+            }
+          }
+          ++tot_save;
+        }
+        uint32_t bw[NW];
+        if (lane == owner) load_words<NW>(p.spec_state, static_cast<int>(Gs), static_cast<int>(col), bw);
+#pragma unroll
+        for (int n = 0; n < NW; ++n) bw[n] = static_cast<uint32_t>(__shfl(static_cast<int>(bw[n]), src, 64));
+        if (lane == rs) {
+#pragma unroll
+          for (int n = 0; n < NW; ++n) w[n] = bw[n];
+        } else if (other) {
+          load_words<NW>(p.spec_state, static_cast<int>(Gs), static_cast<int>(ocol), w);
+        }
+      }
+    } else if constexpr (!kLdsC) {
+      // fanout_kernel's branch kk, this lane: column (s * 16 + kk) * L + lane of planes Spad * 16 * L wide
+      const unsigned Gs = Gpad * kSpecBranches;
+      const unsigned col = (s * kSpecBranches + static_cast<unsigned>(kk)) * L + lane;
+      const CS* __restrict__ scs = reinterpret_cast<const CS*>(p.spec_cs);
+      for (int32_t f = base + 1; f < cur; ++f) {  // the cells adjust would have saved
+        const unsigned slot = static_cast<unsigned>(f % W);
         uint32_t cw[NW];
         load_words<NW>(p.spec_cells + slot * NW * Gs, static_cast<int>(Gs), static_cast<int>(col), cw);
         store_words<NW>(p.snap + slot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), cw);
+        if (lead) {
+          csa[slot * Spad + s] = scs[(slot * Spad + s) * kSpecBranches + kk];
+          p.tag[slot * Spad + s] = f;
+        }
+        ++tot_save;
       }
-      if (lead) {
-        csa[slot * Spad + s] = scs[(slot * Spad + s) * kSpecBranches + kk];
-        p.tag[slot * Spad + s] = f;
-      }
-      ++tot_save;
+      load_words<NW>(p.spec_state, static_cast<int>(Gs), static_cast<int>(col), w);
     }
-    if (real) load_words<NW>(p.spec_state, static_cast<int>(Gs), static_cast<int>(col), w);
     ++tot_sel;
     return true;
   };
@@ -1007,10 +1075,10 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
   // The tick's opening, through the PredictionThreshold decision: 0 = the
   // session stopped on a panic, 1 = the tick is over (Err(PredictionThreshold)),
   // 2 = rollback_and_save, add_local_input and the new frame follow.
-  // The next tick's deliveries are prefetched, except by the fan-out's P2P
-  // launches, which are always of one tick (the fan-out runs between ticks):
-  // there they would only hold registers.
-  constexpr bool kPrefetch = !kSpec;
+  // The next tick's deliveries are prefetched, except by the P2P launches of
+  // the two-launch fan-out (fanout_kernel), which are always of one tick (the
+  // fan-out runs between ticks): there they would only hold registers.
+  constexpr bool kPrefetch = !kSpec || kInFan;
   auto tick_begin = [&](int t) __attribute__((always_inline)) -> int {
     const int tn = t + 1 < p.T ? t + 1 : t;
     if constexpr (kPrefetch) {
@@ -1170,6 +1238,120 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
       q[j].conn_last = q_add(q[j], ring, h, s, cur + p.delay, lin[j]);  // local_connect_status[h].last_frame
     }
   };
+  // ---- the in-kernel fan-out (kInFan, see inlane_fan), after the tick: the
+  // speculated player (the remote handle with the oldest last added input,
+  // ties: the lowest handle), its first unconfirmed frame `base`, and the K
+  // candidates' branches from the saved cell of `base` up to the current
+  // frame, each saving its cells like adjust_gamestate would.  Every lane of
+  // the session runs 16 / L of the branches, kFanGroup at a time.
+  [[maybe_unused]] uint32_t tot_branch = 0;
+  auto fan_inlane = [&]() __attribute__((always_inline)) {
+    if constexpr (kInFan) {
+      const int lane_base = static_cast<int>(__lane_id()) - lane;
+      int rs = -1;
+      int32_t la_rs = INT32_MAX;
+#pragma unroll
+      for (int h = 0; h < P; ++h) {
+        const int32_t la = __shfl(q[0].last_added, lane_base + h, 64);
+        if ((p.local_mask >> h) & 1u) continue;
+        const int32_t key = la == kNullFrame ? -1 : la;
+        if (key < la_rs) {
+          la_rs = key;
+          rs = h;
+        }
+      }
+      const int32_t base = la_rs + 1;
+      const unsigned bslot = static_cast<unsigned>(base >= 0 ? base % W : 0);
+      const int32_t btag = kLdsC ? lds_tag[bslot * bps + sl] : p.tag[bslot * Spad + s];
+      const bool valid = !any_disc && rs >= 0 && base < cur && base + W > cur && base >= 0 && btag == base;
+      // the speculated player's candidates, from its queue's ring (every lane reads the same column)
+      uint32_t cand[4];
+      if constexpr (kLdsQ) {
+        const LdsRing rr{lds_queue + (tid - static_cast<unsigned>(lane) + static_cast<unsigned>(max(rs, 0))), bd};
+        fan_candidates(rr, max(rs, 0), s, la_rs, InputAlphabet<G>::value, p.fan_k, cand);
+      } else {
+        fan_candidates(hbm, max(rs, 0), s, la_rs, InputAlphabet<G>::value, p.fan_k, cand);
+      }
+      sm_valid = valid ? 1 : 0;
+      sm_base = base;
+      sm_end = cur;
+      sm_player = rs;
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) sm_cand[qq] = cand[qq];
+      if (!valid) return;  // session-uniform
+      // the speculated player's words of the base cell (its lane's column), and this lane's own
+      uint32_t bw[NW], ow[NW];
+      if constexpr (kLdsC) {
+#pragma unroll
+        for (int n = 0; n < NW; ++n) {
+          bw[n] = lds_cell[(bslot * NW + n) * bd + tid - static_cast<unsigned>(lane) + static_cast<unsigned>(rs)];
+          ow[n] = lds_cell[(bslot * NW + n) * bd + tid];
+        }
+      } else {
+        load_words<NW>(p.snap + bslot * slot_words, static_cast<int>(Gpad), static_cast<int>(g) - lane + rs, bw);
+        load_words<NW>(p.snap + bslot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), ow);
+      }
+      // Every other player is simulated once from the base cell with the inputs a rollback would
+      // give it (confirmed, or the repeat-last prediction): not always the main trajectory's, which
+      // keeps the effect of predictions a PredictionThreshold tick dropped the rollback of
+      // (p2p_session.rs:320).  Its lane runs it next to its first branch group, into column
+      // Spad * 16 + s * L + lane.
+      const int h_own = min(lane, P - 1);  // (the padding lane of P = 3 reads a real row, unused)
+      const bool other = lane < P && lane != rs;
+      const bool own_local = (p.local_mask >> h_own) & 1u;
+      const int32_t la_own = q[0].last_added;
+      const uint32_t pred_own = la_own == kNullFrame ? 0u : ring.get(la_own, h_own, s);
+      uint32_t vin[kFanPre];
+      fan_prefetch(ring, h_own, s, base, cur, own_local, la_own, pred_own, vin);
+      const uint64_t vpk = fan_pack(vin);
+      const unsigned Gs = Spad * static_cast<unsigned>(kSpecBranches + L);  // branch columns, then the others'
+      const unsigned ocol = Spad * kSpecBranches + s * L + static_cast<unsigned>(lane);
+      constexpr int kB = kSpecBranches / L;  // branches per lane
+#pragma unroll
+      for (int b0 = 0; b0 < kB; b0 += kFanGroup) {
+        uint32_t wb[kFanGroup][NW];
+        InRec in[kFanGroup];
+        bool on[kFanGroup];
+#pragma unroll
+        for (int b = 0; b < kFanGroup; ++b) {
+          const int k = (b0 + b) * L + lane;
+          on[b] = k < p.fan_k;
+          in[b] = static_cast<InRec>(static_cast<uint64_t>(cand_at(cand, k)) << (8 * rs));
+#pragma unroll
+          for (int n = 0; n < NW; ++n) wb[b][n] = bw[n];
+        }
+        const bool run_own = b0 == 0 && other;
+        for (int32_t f = base; f < cur; ++f) {
+          if (f > base) {  // SaveGameState of frame f in every branch
+            const unsigned slot = static_cast<unsigned>(f % W);
+#pragma unroll
+            for (int b = 0; b < kFanGroup; ++b)
+              if (on[b])
+                store_words<NW>(p.spec_cells + slot * NW * Gs, static_cast<int>(Gs),
+                                static_cast<int>(s * kSpecBranches + static_cast<unsigned>((b0 + b) * L + lane)), wb[b]);
+            if (run_own) store_words<NW>(p.spec_cells + slot * NW * Gs, static_cast<int>(Gs), static_cast<int>(ocol), ow);
+          }
+#pragma unroll
+          for (int b = 0; b < kFanGroup; ++b) advance_frame<G>(wb[b], in[b], rs, 0u, &p.counters[1]);
+          if (run_own) {
+            const int j = f - base;
+            uint32_t v;
+            if (j < kFanPre) v = fan_input(vpk, j);
+            else if (own_local || (la_own != kNullFrame && f <= la_own)) v = ring.get(f, h_own, s);  // Confirmed
+            else v = pred_own;  // repeat-last prediction (blank before the first input)
+            advance_frame<G>(ow, static_cast<InRec>(static_cast<uint64_t>(v) << (8 * h_own)), h_own, 0u, &p.counters[1]);
+          }
+        }
+        if (run_own) store_words<NW>(p.spec_state, static_cast<int>(Gs), static_cast<int>(ocol), ow);
+#pragma unroll
+        for (int b = 0; b < kFanGroup; ++b)
+          if (on[b])
+            store_words<NW>(p.spec_state, static_cast<int>(Gs),
+                            static_cast<int>(s * kSpecBranches + static_cast<unsigned>((b0 + b) * L + lane)), wb[b]);
+      }
+      tot_branch += static_cast<uint32_t>(cur - base) * static_cast<uint32_t>(p.fan_k);
+    }
+  };
   auto tick_rotate = [&]() __attribute__((always_inline)) {  // the prefetched deliveries become the next tick's
     if constexpr (kPrefetch) {
 #pragma unroll
@@ -1195,6 +1377,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
       advance(cur);
       next_frame();
     }
+    if (in_fan) fan_inlane();
     tick_rotate();
     return true;
   };
@@ -1324,6 +1507,17 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     p.stats[ST_SAVE * Spad + s] += tot_save;
     p.stats[ST_LOAD * Spad + s] += tot_load;
     p.stats[ST_SELECT * Spad + s] += tot_sel;
+    if constexpr (kInFan) {
+      if (in_fan) {  // the branches' metadata for the next launch's first tick
+        p.stats[ST_BRANCH * Spad + s] += tot_branch;
+        p.spec_meta[SM_BASE * Spad + s] = sm_base;
+        p.spec_meta[SM_END * Spad + s] = sm_end;
+        p.spec_meta[SM_PLAYER * Spad + s] = sm_player;
+        p.spec_meta[SM_VALID * Spad + s] = sm_valid;
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) p.spec_meta[(SM_CAND + qq) * Spad + s] = static_cast<int32_t>(sm_cand[qq]);
+      }
+    }
   }
 }
 
@@ -1445,119 +1639,6 @@ __global__ void __launch_bounds__(256) fanout_kernel(const FanParams p) {
   }
   store_words<NW>(p.spec_state, static_cast<int>(Gs), static_cast<int>(g), w);
   if (k == 0 && lane == 0) p.stats[ST_BRANCH * Spad + s] += static_cast<unsigned long long>(frames) * p.fan_k;
-}
-
-// The fan-out for games whose players move independently (G::kIndependentPlayers,
-// ex_game): the 16 branches differ only in the speculated player's lane, so a
-// session takes 16 + P - 1 lanes — 16 lanes for the speculated player in
-// branches 0-15, then one lane for every other player — instead of 16 x L, and
-// a wave holds 64 / (16 + P - 1) sessions (3 at P = 2..4: 89% of the lanes busy
-// at P = 4).  Cells and states go to column s * LS + k (branch k of the
-// speculated player) or s * LS + 16 + o (the o-th other player, one trajectory
-// for all branches), LS = 16 + P - 1 (indep_cols), of planes Spad * LS wide
-// (the spec buffers hold Spad * 16 * L >= Spad * LS columns); try_select reads
-// that layout.  Each branch cell's
-// checksum is assembled from the branch lane's part and the other players'
-// parts (lane shuffles within the session's lanes).
-template <class G>
-constexpr int indep_session_lanes() {
-  return kSpecBranches + G::kPlayers - 1;
-}
-template <class G>
-constexpr int indep_sessions_per_wave() {
-  return 64 / indep_session_lanes<G>();
-}
-template <class G>
-__global__ void __launch_bounds__(256) fanout_indep_kernel(const FanParams p) {
-  using InRec = typename G::InRec;
-  using CS = typename G::CS;
-  constexpr int NW = G::NWL;
-  constexpr int L = G::kLanes;
-  constexpr int P = G::kPlayers, IB = G::kInputBytes;
-  constexpr int LS = indep_session_lanes<G>(), SPW = indep_sessions_per_wave<G>();
-  static_assert(IndepPlayers<G>::value && L > 1 && LS == indep_cols<G>(), "independent players, one per lane");
-  const unsigned g = blockIdx.x * blockDim.x + threadIdx.x;
-  const int wl = static_cast<int>(g % 64), j = wl / LS, r = wl % LS;
-  if (j >= SPW) return;  // the wave's spare lanes
-  const unsigned s = (g / 64) * SPW + static_cast<unsigned>(j);
-  if (s >= static_cast<unsigned>(p.S)) return;  // the session's lanes leave together
-  const int lane0 = j * LS;                     // the session's first lane in the wave
-  const unsigned Spad = static_cast<unsigned>(p.Spad), Gpad = Spad * L;
-  const unsigned Gs = Spad * static_cast<unsigned>(LS);  // spec plane width in this layout
-  const int W = p.W;
-  const RingIO<IB> ring{const_cast<uint8_t*>(reinterpret_cast<const uint8_t*>(p.ring)), P, p.Spad};
-  auto qrow = [&](int field, int h) { return p.qs[static_cast<size_t>(QS_PLAYER0 + field * 4 + h) * Spad + s]; };
-  const int32_t cur = p.qs[QS_CUR * Spad + s];
-  int rs = -1;  // the remote handle with the oldest last added input (ties: lowest handle), as fanout_kernel
-  int32_t la_rs = INT32_MAX;
-#pragma unroll
-  for (int h = 0; h < P; ++h) {
-    if ((p.local_mask >> h) & 1u) continue;
-    const int32_t la = qrow(QF_LAST_ADDED, h);
-    const int32_t key = la == kNullFrame ? -1 : la;
-    if (key < la_rs) {
-      la_rs = key;
-      rs = h;
-    }
-  }
-  bool any_disc = false;
-#pragma unroll
-  for (int h = 0; h < P; ++h) any_disc |= qrow(QF_DISC, h) != 0;
-  const int32_t base = la_rs + 1;
-  const bool valid = p.status[s] != kP2PStatusPanic && !any_disc && rs >= 0 && base < cur && base + W > cur && base >= 0 &&
-                     p.tag[static_cast<unsigned>(base % W) * Spad + s] == base;
-  uint32_t cand[4];  // the speculated player's candidates (every lane of the session computes the same)
-  fan_candidates(ring, max(rs, 0), s, la_rs, InputAlphabet<G>::value, p.fan_k, cand);
-  if (r == 0) {
-    p.spec_meta[SM_BASE * Spad + s] = base;
-    p.spec_meta[SM_END * Spad + s] = cur;
-    p.spec_meta[SM_PLAYER * Spad + s] = rs;
-    p.spec_meta[SM_VALID * Spad + s] = valid ? 1 : 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) p.spec_meta[(SM_CAND + q) * Spad + s] = static_cast<int32_t>(cand[q]);
-  }
-  if (!valid) return;  // session-uniform
-  const bool branch = r < kSpecBranches;
-  if (branch && r >= p.fan_k) return;  // no candidate for this branch lane
-  const int k = branch ? r : 0;
-  const uint32_t ck = cand_at(cand, k);
-  const int o = r - kSpecBranches;                        // the other players, in handle order, skipping rs
-  const int h = branch ? rs : (o < rs ? o : o + 1);       // this lane's player
-  uint32_t w[NW];
-  load_words<NW>(p.snap + static_cast<unsigned>(base % W) * NW * Gpad, static_cast<int>(Gpad), static_cast<int>(s * L + h), w);
-  const bool local = (p.local_mask >> h) & 1u;
-  const int32_t la_h = qrow(QF_LAST_ADDED, h);
-  const uint32_t pred = la_h == kNullFrame ? 0u : ring.get(la_h, h, s);
-  uint32_t vin[kFanPre];
-  fan_prefetch(ring, h, s, base, cur, local, la_h, pred, vin);
-  const uint64_t vpk = fan_pack(vin);
-  const unsigned col = s * static_cast<unsigned>(LS) + static_cast<unsigned>(r);  // r = k, or 16 + the other-player index
-  CS* __restrict__ cs = reinterpret_cast<CS*>(p.spec_cs);
-  uint32_t frames = 0;
-  for (int32_t f = base; f < cur; ++f) {
-    if (f > base) {  // SaveGameState of frame f in every branch
-      const Fl16 a = G::fan_partial(w, h);
-      uint32_t o1 = 0u, o2 = 0u;  // the other players' parts, read from their lanes
-#pragma unroll
-      for (int q = 0; q < P - 1; ++q) {
-        o1 += static_cast<uint32_t>(__shfl(static_cast<int>(a.s1), lane0 + kSpecBranches + q, 64));
-        o2 += static_cast<uint32_t>(__shfl(static_cast<int>(a.s2), lane0 + kSpecBranches + q, 64));
-      }
-      const unsigned slot = static_cast<unsigned>(f % W);
-      store_words<NW>(p.spec_cells + slot * NW * Gs, static_cast<int>(Gs), static_cast<int>(col), w);
-      if (branch) cs[(slot * Spad + s) * kSpecBranches + k] = G::fan_finish(Fl16{a.s1 + o1, a.s2 + o2}, f);
-    }
-    uint32_t v;
-    const int j = f - base;
-    if (branch) v = ck;
-    else if (j < kFanPre) v = fan_input(vpk, j);
-    else if (local || (la_h != kNullFrame && f <= la_h)) v = ring.get(f, h, s);  // Confirmed
-    else v = pred;  // repeat-last prediction (blank before the first input)
-    advance_frame<G>(w, static_cast<InRec>(static_cast<uint64_t>(v) << (8 * IB * h)), h, 0u, &p.counters[1]);
-    ++frames;
-  }
-  store_words<NW>(p.spec_state, static_cast<int>(Gs), static_cast<int>(col), w);
-  if (r == 0) p.stats[ST_BRANCH * Spad + s] += static_cast<unsigned long long>(frames) * p.fan_k;
 }
 
 }  // namespace rb

@@ -434,10 +434,10 @@ rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs,
     P2P_TRY(b, hipEventRecord(e0, b->stream));
   }
   hipError_t e = hipSuccess;
-  if (!b->fanout) {
-    e = b->ops->launch_p2p(p, b->block, b->stream);  // all ticks in one launch
+  if (!b->fanout || (b->ops->inlane_fanout && !b->fan_generic)) {
+    e = b->ops->launch_p2p(p, b->block, b->stream);  // all ticks in one launch (with the in-kernel fan-out)
   } else {
-    // the fan-out between ticks needs every lane of a session's branches: one
+    // fanout_kernel between ticks needs every lane of a session's branches: one
     // P2P launch and one fan-out launch per tick
     P2PParams pt = p;
     pt.T = 1;

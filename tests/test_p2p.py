@@ -367,9 +367,10 @@ def test_gpu_speculative_fanout_matches_rollback(gpu_available, monkeypatch, cas
     # With the fan-out, matching mispredictions are served by a branch select:
     # statuses, logical request counts, cells and states must stay identical to
     # the reference's rollback (the oracle) on every tick, and selects must
-    # actually happen.  ex_game's players move independently, so the batch runs
-    # fanout_indep_kernel; RB_FANOUT_GENERIC=1 makes it run the generic
-    # fanout_kernel (16 branches x every player) instead.
+    # actually happen.  ex_game's players move independently, so p2p_kernel
+    # runs the fan-out itself (p2p.hpp inlane_fan: the speculated player's
+    # branches only); RB_FANOUT_GENERIC=1 makes the batch run the generic
+    # fanout_kernel (16 branches x every player) as a launch of its own instead.
     import torch
     monkeypatch.setenv("RB_FANOUT_GENERIC", "1" if generic else "0")
     P, W, d, rd, mask, (lo, hi) = case
@@ -426,6 +427,45 @@ def test_gpu_fanout_top_k_candidates_match_rollback(gpu_available, case):
         np.testing.assert_array_equal(ns, ons, err_msg=f"SaveGameState count, tick {t}")
         if t % 10 == 9 or t == T - 1:
             compare_state(sess, orc, t)
+    adv, saves, loads, selects, branch_frames = sess.totals()
+    assert selects > 0, "no misprediction was served by a branch select"
+    assert branch_frames > 0
+    assert sess.counters()[2] == 0 and sess.counters()[1] == 0
+
+
+FANOUT_FUSED_CASES = [  # P, W, d, rd, local_mask, lag range, K, ticks per launch
+    (4, 8, 1, 1, 0b0001, (1, 5), 16, 24),  # config 4's shape; >= 24 ticks: the LDS snapshot ring
+    (4, 8, 1, 1, 0b0001, (1, 5), 6, 7),    # K < 16 (recently confirmed values), HBM cells
+    (2, 8, 2, 2, 0b01, (0, 6), 16, 32),    # 8 branches per lane
+    (3, 7, 0, 0, 0b010, (1, 4), 16, 30),   # the padding lane of a 4-lane group runs branches too
+    (4, 4, 0, 0, 0b0001, (1, 6), 16, 24),  # PredictionThreshold ticks inside the launches
+    (3, 8, 1, 1, 0b001, (1, 5), 5, 40),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", FANOUT_FUSED_CASES, ids=[f"P{c[0]}-W{c[1]}-K{c[6]}-tpl{c[7]}" for c in FANOUT_FUSED_CASES])
+def test_gpu_fanout_fused_launches_match_oracle(gpu_available, case):
+    # The in-kernel fan-out lets one launch hold many ticks (p2p.hpp inlane_fan): the fan-out of
+    # tick t and the select of tick t + 1 run inside the same launch, across launch boundaries
+    # through spec_meta.  After every launch the last tick's request counts and every cell,
+    # state and queue equal the reference's rollback (the oracle), and selects happen.
+    import torch
+    P, W, d, rd, mask, (lo, hi), K, tpl = case
+    S, T = 150, 96
+    inputs, upto, rin = synth_network(S, P, T, mask, rd, lo, hi)
+    di, du, dr = (torch.from_numpy(a).cuda() for a in (inputs, upto, rin))
+    sess, orc = gpu_pair(G.Game.EX_GAME, S, P, W, d, rd, mask, False, fanout=True, candidates=K)
+    for t0 in range(0, T, tpl):
+        t1 = min(T, t0 + tpl)
+        sess.run_ticks(di[t0:t1], du[t0:t1], dr)
+        ost, olf, ona, ons = drive_oracle(orc, mask, inputs, upto, rin, t1, t0=t0)[-1]
+        st, lf, na, ns = sess.status()
+        np.testing.assert_array_equal(st, ost, err_msg=f"status, tick {t1 - 1}")
+        np.testing.assert_array_equal(lf, olf, err_msg=f"rollback frame, tick {t1 - 1}")
+        np.testing.assert_array_equal(na, ona, err_msg=f"AdvanceFrame count, tick {t1 - 1}")
+        np.testing.assert_array_equal(ns, ons, err_msg=f"SaveGameState count, tick {t1 - 1}")
+        compare_state(sess, orc, t1 - 1)
     adv, saves, loads, selects, branch_frames = sess.totals()
     assert selects > 0, "no misprediction was served by a branch select"
     assert branch_frames > 0

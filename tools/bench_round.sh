@@ -4,7 +4,7 @@
 # gpurun_out/bench_<TAG>_<name>.jsonl; stops at the first failing run.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-TAG=${TAG:-r02}
+TAG=${TAG:-r03}
 mkdir -p gpurun_out
 b() {  # b <name> <timeout> <bench args...>
   local name=$1 t=$2; shift 2
@@ -25,7 +25,9 @@ PY
 b driver 300 --gpus 1 --steps 20 --warmup 5 &&
 b synctest 300 --steps 400 --warmup 32 &&
 b brawler 600 --game brawler --steps 100 --warmup 32 &&
+b brawler_tpl1 600 --game brawler --ticks-per-launch 1 --steps 32 --warmup 8 &&
 b p2p 600 --session p2p --steps 400 --warmup 32 &&
-b p2p_sparse 600 --session p2p --sparse-saving --steps 400 --warmup 32 --no-cpu-baseline &&
+b p2p_sparse 600 --session p2p --sparse-saving --steps 400 --warmup 32 &&
 b c4 600 --session p2p --num-players 4 --fanout --steps 100 --warmup 16 &&
+b c4_k8 600 --session p2p --num-players 4 --fanout --fanout-k 8 --steps 100 --warmup 16 --no-cpu-baseline &&
 b wire 600 --session p2p --wire --steps 200 --warmup 32
