@@ -356,18 +356,26 @@ def bench_p2p(args):
     stream = torch.cuda.Stream(device=dev)
     sess.set_stream(stream)
     tpl = args.ticks_per_launch
-    if args.wire:  # receiver-side delivery tensors, filled only by packet decode
+    if args.wire:  # the remote inputs travel as packets: no delivery tensors on the receiver
         import ctypes
         lib = G._lib.load()
         F = dr.shape[0]
-        stride = 64
-        recv = torch.zeros_like(dr)
-        rupto = torch.full((P, S), -1, dtype=torch.int32, device=dev)
-        pk = torch.zeros((S, stride), dtype=torch.uint8, device=dev)
-        ln, st, dst = (torch.zeros(S, dtype=torch.int32, device=dev) for _ in range(3))
+        stride = 32
+        pk = torch.zeros((1, P, S, stride), dtype=torch.uint8, device=dev)
+        ln, st = (torch.zeros((1, P, S), dtype=torch.int32, device=dev) for _ in range(2))
+        acks = torch.full((P, S), -1, dtype=torch.int32, device=dev)  # the receiver's newest frame per endpoint
         ptr = lambda t: ctypes.c_void_p(t.data_ptr())
         sp = ctypes.c_void_p(stream.cuda_stream)
         remotes = [h for h in range(P) if not (mask >> h) & 1]
+        # every call's arguments built ahead (a compiled host's loop): per tick, each remote peer's
+        # send_pending_output since its last ack (device encode), then one launch that decodes the
+        # packets inside the tick's poll and runs the tick (rb_p2p_run_ticks_packets)
+        enc_args = [[(local, sp, h, P, S, 1, ptr(dr), F, args.remote_delay, ptr(acks[h]), ptr(du[t, h]), ptr(pk[0, h]),
+                      stride, ptr(ln[0, h]), ptr(st[0, h])) for h in remotes] for t in range(T)]
+        lstride = P * S * di.element_size()
+        tick_args = [(sess._h, 1, ptr(di[t]), lstride, ptr(pk), stride, ptr(ln), ptr(st), None, ptr(acks))
+                     for t in range(T)]
+        enc, tick_fn = lib.rb_encode_input_packets, lib.rb_p2p_run_ticks_packets
 
     def run(t0, t1):
         if not args.wire:
@@ -375,14 +383,13 @@ def bench_p2p(args):
                 e = min(t1, t + tpl)
                 sess.run_ticks(di[t:e], du[t:e], dr)
             return
+        bad = 0
         for t in range(t0, t1):
-            for h in remotes:  # each remote peer sends what it has since our last receipt; we decode it
-                acked = rupto[h]  # the peer's last acked frame = our newest received (NULL before any)
-                assert lib.rb_encode_input_packets(local, sp, h, P, S, 1, ptr(dr), F, args.remote_delay, ptr(acked),
-                                                   ptr(du[t, h]), ptr(pk), stride, ptr(ln), ptr(st)) == 0
-                assert lib.rb_decode_input_packets(local, sp, h, P, S, 1, W, ptr(pk), stride, ptr(ln), ptr(st),
-                                                   ptr(recv), F, ptr(rupto), ptr(dst)) == 0
-            sess.run_ticks(di[t:t + 1], rupto[None], recv)
+            for a in enc_args[t]:
+                bad |= enc(*a)
+            bad |= tick_fn(*tick_args[t])
+        if bad:
+            raise SystemExit("wire path: a call failed")
 
     with torch.cuda.stream(stream):
         sess.profile_enable(True)  # the warmup takes the timed path (events around every launch)
@@ -452,8 +459,8 @@ def bench_p2p(args):
                                    + (", sparse saving" if args.sparse_saving else "")
                                    + (f", speculative fan-out {K} candidates/frame" if args.fanout else "")
                                    + f", inputs masked 0x{imask:X}"
-                                   + (", inputs delivered as packets (device encode + decode per tick)"
-                                      if args.wire else ""),
+                                   + (", inputs delivered as packets (per tick: the peers' device encode, then "
+                                      "one launch decoding them inside the tick)" if args.wire else ""),
                        "sessions_per_gpu": S, "total_sessions": S * world,
                        "advance_frames_per_session_tick": adv / (S * world * args.steps),
                        "rollbacks_per_session_tick": (loads + selects) / (S * world * args.steps),

@@ -127,6 +127,7 @@ SIGNATURES = [
     ("rb_p2p_set_stream", _I32, [_P, _P]),
     ("rb_p2p_get_stream", _P, [_P]),
     ("rb_p2p_run_ticks", _I32, [_P, _I32, _P, ctypes.c_int64, _P, _P, _I32]),
+    ("rb_p2p_run_ticks_packets", _I32, [_P, _I32, _P, ctypes.c_int64, _P, ctypes.c_int64, _P, _P, _P, _P]),
     ("rb_p2p_read_status", _I32, [_P, _P, _P, _P, _P]),
     ("rb_p2p_disconnect_player", _I32, [_P, _I32, _P]),
     ("rb_p2p_read_frames", _I32, [_P, _P, _P]),

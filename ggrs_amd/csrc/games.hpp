@@ -145,6 +145,13 @@ struct ExGame {
   static constexpr int kCanonWords = 5 * P;
 
   __device__ static uint32_t player_input(InRec rec, int i) { return (static_cast<uint32_t>(rec) >> (8 * i)) & 0xffu; }
+  // The representative of the inputs that move a player alike (p2p.hpp InputCanon): State::advance
+  // reads only up != down and up (thrust, :281-289) and left != right and left (rotation, :291-296),
+  // so the 16 inputs fall into 9 classes (4 bits only: the fan-out's candidates are < 16).
+  __host__ __device__ static constexpr uint32_t canon_input(uint32_t v) {
+    const bool up = v & 1u, down = v & 2u, left = v & 4u, right = v & 8u;
+    return (up != down ? (up ? 1u : 2u) : 0u) | (left != right ? (left ? 4u : 8u) : 0u);
+  }
 
   // ex_game.rs:300-304: if |v| > MAX_SPEED { v = v * MAX_SPEED / |v| }.
   __device__ static void speed_clamp(float& vx, float& vy) {

@@ -754,7 +754,7 @@ struct GameOpsT final : GameOps {
   }
   template <bool kSpec, bool kSparse, bool kNet>
   static hipError_t launch_p2p_as(const P2PParams& p, int grid, int block, hipStream_t st) {
-    size_t lds = p2p_lds_bytes<G>(block);
+    size_t lds = p2p_lds_bytes<G>(block);  // (the HBM-cell launches below)
     if constexpr ((!kSpec || inlane_fan<G>()) && !kNet && p2p_lds_queue<G>()) {
       // the snapshot ring in LDS (p2p_lds_cell_bytes) for launches of many ticks: it is copied in and
       // written back whole, which short launches (the wire path's one tick per launch) do not repay;
@@ -764,7 +764,7 @@ struct GameOpsT final : GameOps {
         // ticks; the fan-out runs lock-step ticks
         auto k = (!p.sync_ticks && !kSpec) ? p2p_kernel<G, kSpec, kSparse, kNet, true, !kSpec>
                                            : p2p_kernel<G, kSpec, kSparse, kNet, true, false>;
-        lds += p2p_lds_cell_bytes<G>(block, p.W);
+        lds = p2p_lds_bytes<G, true>(block) + p2p_lds_cell_bytes<G>(block, p.W);
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                            static_cast<int>(lds));
         if (e != hipSuccess) return e;
@@ -777,6 +777,22 @@ struct GameOpsT final : GameOps {
   }
   hipError_t launch_p2p(const P2PParams& p, int block, hipStream_t st) const override {
     const int grid = (p.Spad * G::kLanes + block - 1) / block;
+    if (p.packets) {  // packet-fed ticks (rb_p2p_run_ticks_packets: the plain path, lock-step ticks)
+      size_t lds = p2p_lds_bytes<G>(block);
+      if constexpr (p2p_lds_queue<G>()) {
+        if (p2p_lds_cells<G>(p.W, block) && p.T >= kLdsCellsMinTicks) {
+          auto k = p2p_kernel<G, false, false, false, true, false, true>;
+          lds = p2p_lds_bytes<G, true>(block) + p2p_lds_cell_bytes<G>(block, p.W);
+          hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             static_cast<int>(lds));
+          if (e != hipSuccess) return e;
+          hipLaunchKernelGGL(k, dim3(grid), dim3(block), lds, st, p);
+          return hipGetLastError();
+        }
+      }
+      hipLaunchKernelGGL((p2p_kernel<G, false, false, false, false, false, true>), dim3(grid), dim3(block), lds, st, p);
+      return hipGetLastError();
+    }
     if (p.ds.interval > 0 || p.peer.on) {  // desync detection / peers' connect-status reports on
       if (p.sparse)  // sparse saving and the fan-out exclude each other (rb_p2p_create)
         return launch_p2p_as<false, true, true>(p, grid, block, st);

@@ -58,6 +58,9 @@ constexpr int kQsFields = QS_PLAYER0 + QF_COUNT * 4;
 // trace rows (the last tick of the last launch): LoadGameState frame, AdvanceFrame count, SaveGameState count
 enum : int { TR_LOAD = 0, TR_NADV = 1, TR_NSAVE = 2, TR_COUNT = 3 };
 constexpr int32_t kP2PStatusOk = 0, kP2PStatusThreshold = 1, kP2PStatusPanic = 101;
+// decode status of a packet-fed tick's endpoint (the codes of wire.hip's rb_decode_input_packets):
+// inputs added, nothing new, malformed (the reference panics, protocol.rs:656), a gap (dropped, :639-642)
+constexpr int32_t kWireOk = 0, kWireNothing = 1, kWirePanic = -1, kWireGap = -2;
 // executed work: AdvanceFrames, SaveGameStates, LoadGameStates, rollbacks
 // replaced by a speculative branch select, branch frames presimulated
 enum : int { ST_ADV = 0, ST_SAVE = 1, ST_LOAD = 2, ST_SELECT = 3, ST_BRANCH = 4, ST_COUNT = 5 };
@@ -182,6 +185,66 @@ __device__ __forceinline__ uint32_t cand_at(const uint32_t (&packed)[4], int k) 
   return (w >> (8 * (k & 3))) & 0xFFu;
 }
 
+// Inputs that act identically on a player's own state (G::canon_input: the
+// game's representative of each class), else every input its own class.  The
+// in-kernel fan-out presimulates one branch per class of its candidates: two
+// candidates of one class give bit-identical trajectories (ex_game's
+// State::advance reads only up != down, up, left != right and left,
+// ex_game.rs:281-296), so a held input selects its class's branch.
+template <class G, class = void>
+struct InputCanon {
+  static constexpr bool value = false;
+  __host__ __device__ static constexpr uint32_t apply(uint32_t v) { return v; }
+};
+template <class G>
+struct InputCanon<G, std::void_t<decltype(G::canon_input(0u))>> {
+  static constexpr bool value = true;
+  __host__ __device__ static constexpr uint32_t apply(uint32_t v) { return G::canon_input(v); }
+};
+// The distinct classes of a whole alphabet of at most kSpecBranches values, in
+// value order, packed like the candidates (0xFF: unused), and their count.
+template <class G>
+struct AlphabetClasses {
+  struct T {
+    uint32_t packed[4];
+    int n;
+  };
+  static constexpr T make() {
+    T t{{~0u, ~0u, ~0u, ~0u}, 0};
+    constexpr uint32_t A = InputAlphabet<G>::value;
+    for (uint32_t v = 0; v < A && v < static_cast<uint32_t>(kSpecBranches); ++v) {
+      const uint32_t c = InputCanon<G>::apply(v) & 0xFFu;
+      bool seen = false;
+      for (int i = 0; i < t.n; ++i) seen = seen || ((t.packed[i >> 2] >> (8 * (i & 3))) & 0xFFu) == c;
+      if (!seen) {
+        t.packed[t.n >> 2] = (t.packed[t.n >> 2] & ~(0xFFu << (8 * (t.n & 3)))) | (c << (8 * (t.n & 3)));
+        ++t.n;
+      }
+    }
+    return t;
+  }
+  static constexpr T value = make();
+};
+// The classes of the first K packed candidates, deduplicated in candidate
+// order (the branches of the in-kernel fan-out); returns their count.
+template <class G>
+__device__ __forceinline__ int cand_classes(const uint32_t (&cand)[4], int K, uint32_t (&cls)[4]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) cls[q] = ~0u;
+  int n = 0;
+#pragma unroll
+  for (int i = 0; i < kSpecBranches; ++i) {
+    const uint32_t c = InputCanon<G>::apply(cand_at(cand, i)) & 0xFFu;
+    if (i < K && cand_find(cls, c, n) < 0) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        cls[q] = (n >> 2) == q ? ((cls[q] & ~(0xFFu << (8 * (n & 3)))) | (c << (8 * (n & 3)))) : cls[q];
+      ++n;
+    }
+  }
+  return n;
+}
+
 // ---------------------------------------------------------------------------
 // Desync detection (p2p_session.rs:154-157, 313-316, 873-928; the UdpProtocol
 // side: protocol.rs:27, 176-178, 710-742).  Per session, all of it touched
@@ -265,6 +328,17 @@ struct P2PParams {
   int32_t sync_ticks;  // 1: lock-step ticks on the plain path too (no kAsync; A/B and tests)
   DesyncParams ds;
   PeerParams peer;
+  // kWire (rb_p2p_run_ticks_packets): the remote inputs arrive as the peers'
+  // input packets (wire.hip's format), decoded inside the tick instead of the
+  // delivery tensors above.  Tick t, remote handle h, session s: the packet at
+  // packets + ((t * P + h) * S + s) * packet_stride, its length and start frame
+  // at pk_len / pk_start[(t * P + h) * S + s].
+  const uint8_t* packets;
+  int64_t packet_stride;
+  const int32_t* pk_len;
+  const int32_t* pk_start;
+  int32_t* pk_status;  // [P][S] the last tick's decode status per endpoint (wire.hip codes), or null
+  int32_t* acks;       // [P][S] after the launch: the newest frame received per endpoint (the ack), or null
 };
 
 // The cells as check_checksum_send_interval sees them.  It runs inside
@@ -445,9 +519,21 @@ template <class G>
 constexpr bool p2p_lds_queue() {
   return G::kInputBytes == 1 && (G::kLanes > 1 || G::kPlayers == 1);
 }
-template <class G>
+// ... in a launch whose snapshot ring is (kLdsC) or is not in LDS.  Launches of
+// few ticks keep the snapshot ring in HBM, and the input ring too: filling the
+// LDS copy (byte loads in dependent rounds) and writing it back cost more than
+// the handful of ring reads a short launch makes (measured, one tick per
+// launch at 65,536 sessions: 14.8 -> 13.1 us, the packet-fed tick 18.9 -> 16.7).
+#ifndef RB_SHORT_HBM_RING
+#define RB_SHORT_HBM_RING 1  // 0: the LDS input ring in every launch (A/B builds)
+#endif
+template <class G, bool kLdsC>
+constexpr bool p2p_lds_queue_in() {
+  return p2p_lds_queue<G>() && (kLdsC || !RB_SHORT_HBM_RING);
+}
+template <class G, bool kLdsC = false>
 constexpr size_t p2p_lds_bytes(int block) {
-  return p2p_lds_queue<G>() ? static_cast<size_t>(kQueueLen) * static_cast<size_t>(block) : 0;
+  return p2p_lds_queue_in<G, kLdsC>() ? static_cast<size_t>(kQueueLen) * static_cast<size_t>(block) : 0;
 }
 // The snapshot ring in LDS (p2p_kernel kLdsC): for the launch, the W cells
 // (words [W][NWL][block], frame tags and checksums [W][block / kLanes]) live
@@ -479,7 +565,7 @@ constexpr int kLdsCellsMinTicks = RB_LDS_CELLS_MIN_TICKS;
 template <class G>
 constexpr bool p2p_lds_cells(int W, int block) {
   return p2p_lds_queue<G>() && W <= kLdsCellsMaxW &&
-         p2p_lds_bytes<G>(block) + p2p_lds_cell_bytes<G>(block, W) <= kLdsPerBlockMax;
+         p2p_lds_bytes<G, true>(block) + p2p_lds_cell_bytes<G>(block, W) <= kLdsPerBlockMax;
 }
 
 // input_queue.rs:167-204 add_input_by_frame
@@ -568,6 +654,14 @@ constexpr bool inlane_fan() {
   else return false;
 }
 constexpr int kFanGroup = 4;  // branches a lane advances together (its independent chains)
+#ifndef RB_FAN_INRANGE
+#define RB_FAN_INRANGE 1  // 0: the fan-out's chains always take the general AdvanceFrame (A/B builds)
+#endif
+// Attribution builds only (tools/mkvar.sh -DRB_FAN_EXP=...; results are wrong): 1 presimulates no
+// branch (every fan-out invalid), 2 stores no branch cell.  Always 0 in the product.
+#ifndef RB_FAN_EXP
+#define RB_FAN_EXP 0
+#endif
 
 // kSpec / kSparse / kNet: the fan-out select, sparse saving and the
 // network-fed bookkeeping (desync detection, peers' connect-status reports)
@@ -593,9 +687,10 @@ constexpr int kFanGroup = 4;  // branches a lane advances together (its independ
 // operations run in the reference's order, except that the tick's final
 // SaveGameState moves behind set_last_confirmed_frame and add_local_input,
 // which touch neither the state nor the cells.
-template <class G, bool kSpec, bool kSparse, bool kNet, bool kLdsC, bool kAsync>
+template <class G, bool kSpec, bool kSparse, bool kNet, bool kLdsC, bool kAsync, bool kWire = false>
 __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
   static_assert(!kAsync || (kLdsC && !kSpec && !kNet), "lane-asynchronous ticks: plain or sparse path, LDS cells");
+  static_assert(!kWire || (!kSpec && !kSparse && !kNet && !kAsync), "packet-fed ticks: the plain lock-step path");
   using InRec = typename G::InRec;
   using CS = typename G::CS;
   constexpr int NW = G::NWL;
@@ -617,7 +712,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
   const unsigned slot_words = static_cast<unsigned>(NW) * Gpad;
   const int W = p.W;
   CS* __restrict__ csa = reinterpret_cast<CS*>(p.cs);
-  constexpr bool kLdsQ = p2p_lds_queue<G>();
+  constexpr bool kLdsQ = p2p_lds_queue_in<G, kLdsC>();
   const RingIO<IB> hbm{reinterpret_cast<uint8_t*>(p.ring), P, p.Spad};
   extern __shared__ uint8_t lds_queue[];
   const auto ring = [&]() __attribute__((always_inline)) {
@@ -693,7 +788,8 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
   const int32_t la0 = q[0].last_added;
   if constexpr (kLdsQ) {
     const int h = player_of(0);
-    const int32_t back = (in_fan && InputAlphabet<G>::value > static_cast<uint32_t>(p.fan_k)) ? 32 : 0;
+    // (and a packet's reference input, frame start - 1 >= last received - 2 * max_prediction)
+    const int32_t back = kWire ? 2 * W + 1 : ((in_fan && InputAlphabet<G>::value > static_cast<uint32_t>(p.fan_k)) ? 32 : 0);
     if (h < P && la0 != kNullFrame) {
       const int32_t lo = max(max(0, la0 - (kQueueLen - 1)), min(cur - W, la0) - back);
       for (int32_t f0 = lo; f0 <= la0; f0 += 8) {  // 8 loads in flight per round trip
@@ -845,7 +941,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
   auto try_select = [&](int32_t first_incorrect, int32_t min_confirmed) __attribute__((always_inline)) -> bool {
     if (kLdsC && !in_fan) return false;  // (not launched: fanout_kernel's branches need HBM cells)
     if (any_disc || disc_frame != kNullFrame) return false;  // the branches assumed everybody connected
-    if (!sm_valid || sm_end != cur) return false;
+    if (!(sm_valid & 1) || sm_end != cur) return false;
     const int32_t base = sm_base;
     const int rs = sm_player;
     if (first_incorrect != base || base + W <= cur) return false;
@@ -865,7 +961,8 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     }
     // the lane that owns the speculated player found the held value k; its branch is the candidate
     // slot holding k (none: no branch presimulated it); share it with the group
-    int32_t kk = cand_find(sm_cand, k, p.fan_k);
+    // (the in-kernel fan-out's branches are the candidates' classes, sm_valid >> 8 of them)
+    int32_t kk = in_fan ? cand_find(sm_cand, InputCanon<G>::apply(k) & 0xFFu, sm_valid >> 8) : cand_find(sm_cand, k, p.fan_k);
     kk = (kSplit ? lane == rs : true) ? kk : -1;
     kk = -group_min<L>(-kk);  // max over the group
     ok = group_min<L>(ok ? 1 : 0) == 1;
@@ -1019,6 +1116,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
   constexpr int kPre = 4;
   const int first_local = p.local_mask ? __builtin_ctz(p.local_mask) : 0;
   auto load_upto = [&](int t, int j) __attribute__((always_inline)) -> int32_t {
+    if constexpr (kWire) return kNullFrame;  // (no delivery tensors: packets)
     const int h = min(player_of(j), P - 1);
     return p.upto[static_cast<int64_t>(t) * p.upto_stride + static_cast<int64_t>(h) * p.S + s];
   };
@@ -1038,8 +1136,9 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
   const uint8_t* rbase[PPL];
 #pragma unroll
   for (int j = 0; j < PPL; ++j)
-    rbase[j] = p.remote_in + (static_cast<size_t>(min(player_of(j), P - 1)) * p.S + s) * IB;
+    rbase[j] = kWire ? nullptr : p.remote_in + (static_cast<size_t>(min(player_of(j), P - 1)) * p.S + s) * IB;
   auto load_remote = [&](int j, int32_t f) __attribute__((always_inline)) -> uint32_t {
+    if constexpr (kWire) return 0u;
     f = max(0, min(f, p.remote_frames - 1));
     const uint8_t* src = rbase[j] + static_cast<uint64_t>(static_cast<uint32_t>(f)) * rstride;
     return IB == 4 ? *reinterpret_cast<const uint32_t*>(src) : *src;
@@ -1068,6 +1167,114 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     for (int k = 0; k < kPre; ++k) rv[j][k] = load_remote(j, f + k);
   }
 
+  // ---- kWire: UdpProtocol::on_input (protocol.rs:616-689) for the endpoint
+  // of remote handle h, fused into the poll.  The packet is the XOR delta of
+  // its inputs against the input before its start frame, bitfield-RLE coded
+  // (network/compression.rs, wire.hip); that reference input is the queue's
+  // ring entry of frame start - 1 (recv_inputs holds what the queue holds:
+  // remote inputs enter it at their own frame).  A structurally invalid packet
+  // adds nothing and panics the session, as the reference's decode().expect
+  // does; a first pass validates, the second adds every input past the last
+  // received frame.  The first 32 bytes come in as 8 words (a byte window
+  // shifted as it is consumed), later bytes one load each.
+  [[maybe_unused]] auto wire_poll = [&](int j, int h, int t) __attribute__((always_inline)) -> int32_t {
+    if constexpr (!kWire) {
+      return kWireNothing;
+    } else {
+      const size_t idx = (static_cast<size_t>(t) * P + static_cast<size_t>(h)) * static_cast<size_t>(p.S) + s;
+      const int32_t n = p.pk_len[idx], start = p.pk_start[idx];
+      const uint8_t* pk = p.packets + static_cast<int64_t>(idx) * p.packet_stride;
+      uint32_t w0[8];
+      {
+        const uint4 a = reinterpret_cast<const uint4*>(pk)[0], b = reinterpret_cast<const uint4*>(pk)[1];
+        w0[0] = a.x, w0[1] = a.y, w0[2] = a.z, w0[3] = a.w, w0[4] = b.x, w0[5] = b.y, w0[6] = b.z, w0[7] = b.w;
+      }
+      if (q[j].disc || n <= 0) return kWireNothing;  // a disconnected player's endpoint no longer runs
+      const int32_t last = q[j].conn_last;
+      if (last != kNullFrame && last + 1 < start) return kWireGap;
+      if (last != kNullFrame && (start - 1 < last - 2 * W || start - 1 < kNullFrame)) return kWireNothing;
+      const uint32_t ref = (last != kNullFrame && start - 1 != kNullFrame) ? ring.get(start - 1, h, s) : 0u;
+      // pass 0 validates (and counts the bytes the inputs take), pass 1 adds the inputs
+      int32_t nbytes = 0;
+      for (int pass = 0; pass < 2; ++pass) {
+        uint32_t win[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) win[i] = w0[i];
+        int32_t pos = 0, k = 0;
+        uint32_t acc = 0;
+        auto next = [&]() __attribute__((always_inline)) -> uint32_t {
+          const uint32_t b = pos < 32 ? (win[0] & 0xFFu) : pk[pos];
+#pragma unroll
+          for (int i = 0; i < 7; ++i) win[i] = __builtin_amdgcn_alignbyte(win[i + 1], win[i], 1);
+          win[7] >>= 8;
+          ++pos;
+          return b;
+        };
+        auto emit = [&](uint32_t x) __attribute__((always_inline)) {
+          const int i = k % IB;
+          acc |= (((ref >> (8 * i)) ^ x) & 0xFFu) << (8 * i);
+          if (i == IB - 1) {
+            const int32_t f = start + k / IB;
+            if (f > last) {  // protocol.rs:661-663: inputs already received are skipped
+              q_add(q[j], ring, h, s, f, acc);  // add_remote_input (frame delay 0)
+              q[j].conn_last = f;
+            }
+            acc = 0;
+          }
+          ++k;
+        };
+        bool ok = true;
+        while (pos < n) {
+          uint32_t hdr = 0;
+          int shift = 0;
+          bool done = false;
+          while (pos < n && shift < 35) {  // LEB128
+            const uint32_t b = next();
+            hdr |= (b & 0x7Fu) << shift;
+            shift += 7;
+            if (!(b & 0x80u)) {
+              done = true;
+              break;
+            }
+          }
+          if (!done) {
+            ok = false;
+            break;
+          }
+          if (hdr & 1u) {  // a run of 0x00 / 0xFF bytes
+            const uint32_t len = hdr >> 2;
+            if (len > (1u << 16)) {
+              ok = false;
+              break;
+            }
+            if (pass == 0) {
+              k += static_cast<int32_t>(len);
+            } else {
+              const uint32_t x = (hdr & 2u) ? 0xFFu : 0u;
+              for (uint32_t i = 0; i < len; ++i) emit(x);
+            }
+          } else {  // literal bytes
+            const uint32_t len = hdr >> 1;
+            if (len > static_cast<uint32_t>(n - pos)) {
+              ok = false;
+              break;
+            }
+            for (uint32_t i = 0; i < len; ++i) {
+              const uint32_t x = next();
+              if (pass == 1) emit(x);
+              else ++k;
+            }
+          }
+        }
+        if (pass == 0) {
+          if (!ok || k % IB != 0) return kWirePanic;  // compression.rs:47: whole inputs only
+          nbytes = k;
+        }
+      }
+      return start + nbytes / IB - 1 > last ? kWireOk : kWireNothing;
+    }
+  };
+
   // One tick of the batch for this session (advance_frame and the requests it
   // returns); false when the session stops on a reference panic.
   int32_t up_n[PPL];
@@ -1095,6 +1302,14 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
 #pragma unroll
     for (int j = 0; j < PPL; ++j) {
       const int h = player_of(j);
+      if constexpr (kWire) {
+        if (h < P && !((p.local_mask >> h) & 1u)) {
+          const int32_t ds = wire_poll(j, h, t);
+          if (p.pk_status) p.pk_status[static_cast<size_t>(h) * p.S + s] = ds;
+          if (ds == kWirePanic) status = kP2PStatusPanic;  // the reference panics ("decoding failed")
+        }
+        continue;
+      }
       if (h < P && !((p.local_mask >> h) & 1u) && !q[j].disc) {  // handle_event ignores a disconnected player (:852)
         const int32_t end = min(up[j], p.remote_frames - 1);
         int32_t f = remote_start(j);
@@ -1121,7 +1336,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     {  // input_queue.rs:181 assert!(self.length <= INPUT_QUEUE_LENGTH) fired during the poll.  No
       // branch here: the panic status is picked up by the panic check after the threshold decision
       // (a branch at this point would make the waitcnt pass wait for the loads in flight).
-      bool ovf = false;
+      bool ovf = kWire && status == kP2PStatusPanic;  // (a malformed packet, decoded by its player's lane)
 #pragma unroll
       for (int j = 0; j < PPL; ++j) ovf |= q_overflow(q[j]);
       status = group_min<L>(ovf ? 0 : 1) == 0 ? kP2PStatusPanic : status;
@@ -1263,16 +1478,28 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
       const int32_t base = la_rs + 1;
       const unsigned bslot = static_cast<unsigned>(base >= 0 ? base % W : 0);
       const int32_t btag = kLdsC ? lds_tag[bslot * bps + sl] : p.tag[bslot * Spad + s];
-      const bool valid = !any_disc && rs >= 0 && base < cur && base + W > cur && base >= 0 && btag == base;
-      // the speculated player's candidates, from its queue's ring (every lane reads the same column)
+      const bool valid = !(RB_FAN_EXP & 1) && !any_disc && rs >= 0 && base < cur && base + W > cur && base >= 0 && btag == base;
+      // the speculated player's candidates, from its queue's ring (every lane reads the same column),
+      // as their distinct classes (InputCanon): one branch per class.  A whole alphabet of at most K
+      // values gives a compile-time set.
       uint32_t cand[4];
-      if constexpr (kLdsQ) {
-        const LdsRing rr{lds_queue + (tid - static_cast<unsigned>(lane) + static_cast<unsigned>(max(rs, 0))), bd};
-        fan_candidates(rr, max(rs, 0), s, la_rs, InputAlphabet<G>::value, p.fan_k, cand);
+      int nb;
+      if (InputAlphabet<G>::value <= static_cast<uint32_t>(p.fan_k)) {
+        constexpr auto AC = AlphabetClasses<G>::value;
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) cand[qq] = AC.packed[qq];
+        nb = AC.n;
       } else {
-        fan_candidates(hbm, max(rs, 0), s, la_rs, InputAlphabet<G>::value, p.fan_k, cand);
+        uint32_t raw[4];
+        if constexpr (kLdsQ) {
+          const LdsRing rr{lds_queue + (tid - static_cast<unsigned>(lane) + static_cast<unsigned>(max(rs, 0))), bd};
+          fan_candidates(rr, max(rs, 0), s, la_rs, InputAlphabet<G>::value, p.fan_k, raw);
+        } else {
+          fan_candidates(hbm, max(rs, 0), s, la_rs, InputAlphabet<G>::value, p.fan_k, raw);
+        }
+        nb = cand_classes<G>(raw, p.fan_k, cand);
       }
-      sm_valid = valid ? 1 : 0;
+      sm_valid = valid ? (1 | (nb << 8)) : 0;  // (the branch count rides along)
       sm_base = base;
       sm_end = cur;
       sm_player = rs;
@@ -1307,6 +1534,19 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
       const unsigned Gs = Spad * static_cast<unsigned>(kSpecBranches + L);  // branch columns, then the others'
       const unsigned ocol = Spad * kSpecBranches + s * L + static_cast<unsigned>(lane);
       constexpr int kB = kSpecBranches / L;  // branches per lane
+      // every chain of the wave starts in range (games.hpp in_range: e.g. ex_game rotations in [+0, 6.5),
+      // which stay there for any number of frames): the AdvanceFrames skip the out-of-range library paths
+      bool inr = false;
+      if constexpr (G::kHasRangePath && RB_FAN_INRANGE) inr = __all(G::in_range(bw) && G::in_range(ow));
+      auto adv = [&](uint32_t (&x)[NW], InRec in, int pl) __attribute__((always_inline)) {
+        if constexpr (G::kHasRangePath) {
+          if (inr) {
+            G::template advance<true>(x, in, pl, 0u, &p.counters[1]);
+            return;
+          }
+        }
+        advance_frame<G>(x, in, pl, 0u, &p.counters[1]);
+      };
 #pragma unroll
       for (int b0 = 0; b0 < kB; b0 += kFanGroup) {
         uint32_t wb[kFanGroup][NW];
@@ -1315,14 +1555,14 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
 #pragma unroll
         for (int b = 0; b < kFanGroup; ++b) {
           const int k = (b0 + b) * L + lane;
-          on[b] = k < p.fan_k;
+          on[b] = k < nb;
           in[b] = static_cast<InRec>(static_cast<uint64_t>(cand_at(cand, k)) << (8 * rs));
 #pragma unroll
           for (int n = 0; n < NW; ++n) wb[b][n] = bw[n];
         }
         const bool run_own = b0 == 0 && other;
         for (int32_t f = base; f < cur; ++f) {
-          if (f > base) {  // SaveGameState of frame f in every branch
+          if (f > base && !(RB_FAN_EXP & 2)) {  // SaveGameState of frame f in every branch
             const unsigned slot = static_cast<unsigned>(f % W);
 #pragma unroll
             for (int b = 0; b < kFanGroup; ++b)
@@ -1332,14 +1572,14 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
             if (run_own) store_words<NW>(p.spec_cells + slot * NW * Gs, static_cast<int>(Gs), static_cast<int>(ocol), ow);
           }
 #pragma unroll
-          for (int b = 0; b < kFanGroup; ++b) advance_frame<G>(wb[b], in[b], rs, 0u, &p.counters[1]);
+          for (int b = 0; b < kFanGroup; ++b) adv(wb[b], in[b], rs);
           if (run_own) {
             const int j = f - base;
             uint32_t v;
             if (j < kFanPre) v = fan_input(vpk, j);
             else if (own_local || (la_own != kNullFrame && f <= la_own)) v = ring.get(f, h_own, s);  // Confirmed
             else v = pred_own;  // repeat-last prediction (blank before the first input)
-            advance_frame<G>(ow, static_cast<InRec>(static_cast<uint64_t>(v) << (8 * h_own)), h_own, 0u, &p.counters[1]);
+            adv(ow, static_cast<InRec>(static_cast<uint64_t>(v) << (8 * h_own)), h_own);
           }
         }
         if (run_own) store_words<NW>(p.spec_state, static_cast<int>(Gs), static_cast<int>(ocol), ow);
@@ -1349,7 +1589,7 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
             store_words<NW>(p.spec_state, static_cast<int>(Gs),
                             static_cast<int>(s * kSpecBranches + static_cast<unsigned>((b0 + b) * L + lane)), wb[b]);
       }
-      tot_branch += static_cast<uint32_t>(cur - base) * static_cast<uint32_t>(p.fan_k);
+      tot_branch += static_cast<uint32_t>(cur - base) * static_cast<uint32_t>(nb);
     }
   };
   auto tick_rotate = [&]() __attribute__((always_inline)) {  // the prefetched deliveries become the next tick's
@@ -1492,6 +1732,15 @@ __global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
     *qrow(QF_TAIL, h) = q[j].tail;
     *qrow(QF_LEN, h) = q[j].len;
     if constexpr (kNet) *qrow(QF_DISC, h) = q[j].disc ? 1 : 0;  // update_player_disconnects may set it
+  }
+  if constexpr (kWire) {  // the newest frame received per endpoint: what the receiver acks
+    if (p.acks) {
+#pragma unroll
+      for (int j = 0; j < PPL; ++j) {
+        const int h = player_of(j);
+        if (h < P && !((p.local_mask >> h) & 1u)) p.acks[static_cast<size_t>(h) * p.S + s] = q[j].conn_last;
+      }
+    }
   }
   if (lead) {
     p.qs[QS_CUR * Spad + s] = cur;

@@ -362,11 +362,9 @@ void* rb_p2p_get_stream(const rb_p2p* b) { return static_cast<void*>(b->stream);
 int32_t rb_p2p_state_bytes(const rb_p2p* b) { return b->ops->image_bytes; }
 int32_t rb_p2p_input_bytes(const rb_p2p* b) { return b->ops->input_bytes; }
 
-rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs, int64_t local_stride,
-                           const int32_t* remote_upto, const void* remote_inputs, int32_t remote_frames) {
-  if (n_ticks <= 0) return RB_OK;
-  if (!local_inputs || !remote_upto || !remote_inputs || remote_frames <= 0)
-    return pfail(b, RB_INVALID_REQUEST, "rb_p2p_run_ticks: missing input tensor");
+namespace {
+// The batch's buffers and configuration for a P2P launch (the per-call tensors are the caller's).
+P2PParams base_params(const rb_p2p* b) {
   P2PParams p{};
   p.snap = b->snap;
   p.cs = b->cs;
@@ -378,18 +376,11 @@ rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs,
   p.trace = b->trace;
   p.counters = b->counters;
   p.stats = b->stats;
-  p.local_in = static_cast<const uint8_t*>(local_inputs);
-  p.local_stride = local_stride;
-  p.upto = remote_upto;
-  p.upto_stride = static_cast<int64_t>(b->P) * b->S;
-  p.remote_in = static_cast<const uint8_t*>(remote_inputs);
-  p.remote_frames = remote_frames;
   p.S = b->S;
   p.Spad = b->Spad;
   p.W = b->W;
   p.delay = b->cfg.input_delay;
   p.remote_delay = b->cfg.remote_delay;
-  p.T = n_ticks;
   p.local_mask = b->cfg.local_mask;
   p.sparse = b->cfg.sparse_saving != 0;
   p.sync_ticks = b->sync_ticks ? 1 : 0;
@@ -402,6 +393,23 @@ rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs,
   p.spec_meta = b->spec_meta;
   p.ds = b->ds;
   p.peer = b->peer;
+  return p;
+}
+}  // namespace
+
+rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs, int64_t local_stride,
+                           const int32_t* remote_upto, const void* remote_inputs, int32_t remote_frames) {
+  if (n_ticks <= 0) return RB_OK;
+  if (!local_inputs || !remote_upto || !remote_inputs || remote_frames <= 0)
+    return pfail(b, RB_INVALID_REQUEST, "rb_p2p_run_ticks: missing input tensor");
+  P2PParams p = base_params(b);
+  p.local_in = static_cast<const uint8_t*>(local_inputs);
+  p.local_stride = local_stride;
+  p.upto = remote_upto;
+  p.upto_stride = static_cast<int64_t>(b->P) * b->S;
+  p.remote_in = static_cast<const uint8_t*>(remote_inputs);
+  p.remote_frames = remote_frames;
+  p.T = n_ticks;
   FanParams fp{};
   fp.status = b->status;
   fp.snap = b->snap;
@@ -450,6 +458,46 @@ rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs,
   }
   if (e != hipSuccess) return pfail(b, RB_DEVICE_ERROR, std::string("p2p launch: ") + hipGetErrorString(e));
   if (b->prof) P2P_TRY(b, hipEventRecord(e1, b->stream));
+  return RB_OK;
+}
+
+rb_status rb_p2p_run_ticks_packets(rb_p2p* b, int32_t n_ticks, const void* local_inputs, int64_t local_stride,
+                                   const uint8_t* packets, int64_t packet_stride, const int32_t* lengths,
+                                   const int32_t* start_frames, int32_t* decode_status, int32_t* acks) {
+  if (n_ticks <= 0) return RB_OK;
+  if (!local_inputs || !packets || !lengths || !start_frames)
+    return pfail(b, RB_INVALID_REQUEST, "rb_p2p_run_ticks_packets: missing input tensor");
+  if (packet_stride < 32 || packet_stride % 16 != 0 || reinterpret_cast<uintptr_t>(packets) % 16 != 0)
+    return pfail(b, RB_INVALID_REQUEST, "rb_p2p_run_ticks_packets: packets need 16-byte alignment and a stride of at least 32");
+  if (b->cfg.sparse_saving || b->fanout || b->ds.interval > 0 || b->peer.on)
+    return pfail(b, RB_INVALID_REQUEST,
+                 "rb_p2p_run_ticks_packets: sparse saving, the fan-out and network reports take rb_p2p_run_ticks");
+  P2PParams p = base_params(b);
+  p.local_in = static_cast<const uint8_t*>(local_inputs);
+  p.local_stride = local_stride;
+  p.T = n_ticks;
+  p.packets = packets;
+  p.packet_stride = packet_stride;
+  p.pk_len = lengths;
+  p.pk_start = start_frames;
+  p.pk_status = decode_status;
+  p.acks = acks;
+  P2P_TRY(b, hipSetDevice(b->device));
+  hipEvent_t e1 = nullptr;
+  if (b->prof) {
+    if (b->prof_used == b->prof_ev.size()) {
+      hipEvent_t e0 = nullptr, e2 = nullptr;
+      P2P_TRY(b, hipEventCreate(&e0));
+      P2P_TRY(b, hipEventCreate(&e2));
+      b->prof_ev.emplace_back(e0, e2);
+    }
+    P2P_TRY(b, hipEventRecord(b->prof_ev[b->prof_used].first, b->stream));
+    e1 = b->prof_ev[b->prof_used].second;
+    ++b->prof_used;
+  }
+  hipError_t e = b->ops->launch_p2p(p, b->block, b->stream);
+  if (e != hipSuccess) return pfail(b, RB_DEVICE_ERROR, std::string("p2p launch: ") + hipGetErrorString(e));
+  if (e1) P2P_TRY(b, hipEventRecord(e1, b->stream));
   return RB_OK;
 }
 

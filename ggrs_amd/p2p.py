@@ -77,6 +77,8 @@ class P2PSession(_StreamOrdered):
     def _check(self, st):
         if st != L.RB_OK:
             msg = (self._lib.rb_p2p_last_error(self._h) or b"").decode()
+            if st == L.RB_INVALID_REQUEST:
+                raise InvalidRequest(msg)
             raise DeviceError(msg) if st == L.RB_DEVICE_ERROR else Panic(msg)
 
     def local_player_handles(self):  # p2p_session.rs:416-419
@@ -108,6 +110,40 @@ class P2PSession(_StreamOrdered):
         stride = self.num_players * self.num_sessions * lk.element_size()
         self._check(self._lib.rb_p2p_run_ticks(self._h, T, lp, stride, up, rp, int(remote_inputs.shape[0])))
         self._post(cur, (lk, uk, rk))
+
+    def run_ticks_packets(self, local_inputs, packets, lengths, start_frames, decode_status=None, acks=None) -> None:
+        """T ticks fed by the peers' input packets (rb_p2p_run_ticks_packets):
+        each tick decodes every remote endpoint's packet inside its poll
+        (UdpProtocol::on_input), then runs as run_ticks.
+
+        local_inputs  [T, P, S] Input values (remote handles' rows ignored)
+        packets       [T, P, S, stride] uint8 (stride a multiple of 16, >= 32)
+        lengths, start_frames [T, P, S] int32 (length 0: no packet)
+        decode_status, acks   None or [P, S] int32 outputs: the last tick's decode
+                      result per endpoint, the newest frame received per endpoint"""
+        T = int(local_inputs.shape[0])
+        assert tuple(local_inputs.shape[1:]) == (self.num_players, self.num_sessions)
+        assert tuple(packets.shape[:3]) == (T, self.num_players, self.num_sessions) and packets.dim() == 4
+        assert tuple(lengths.shape) == tuple(start_frames.shape) == (T, self.num_players, self.num_sessions)
+        lp, lk = _dev_ptr(local_inputs)
+        pp, pk = _dev_ptr(packets)
+        np_, nk = _dev_ptr(lengths)
+        sp, sk = _dev_ptr(start_frames)
+        keep = [lk, pk, nk, sk]
+        outs = []
+        for o in (decode_status, acks):
+            if o is None:
+                outs.append(None)
+            else:
+                assert tuple(o.shape) == (self.num_players, self.num_sessions) and o.is_contiguous()
+                op, ok = _dev_ptr(o)
+                outs.append(op)
+                keep.append(ok)
+        cur = self._pre()
+        stride = self.num_players * self.num_sessions * lk.element_size()
+        self._check(self._lib.rb_p2p_run_ticks_packets(self._h, T, lp, stride, pp, int(packets.shape[3]), np_, sp,
+                                                       outs[0], outs[1]))
+        self._post(cur, tuple(keep), outputs=decode_status is not None or acks is not None)
 
     def disconnect_player(self, handle: int, sessions=None) -> None:
         """P2PSession::disconnect_player(handle) (p2p_session.rs:430-456) in every

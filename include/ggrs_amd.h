@@ -295,6 +295,30 @@ void* rb_p2p_get_stream(const rb_p2p* b);  /* as rb_get_stream */
 rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs, int64_t local_stride_bytes,
                            const int32_t* remote_upto, const void* remote_inputs, int32_t remote_frames);
 
+/* rb_p2p_run_ticks with the remote inputs arriving as the peers' input packets
+ * (the format of rb_encode_input_packets below): each tick first runs
+ * UdpProtocol::on_input (protocol.rs:616-689) for every remote endpoint inside
+ * the tick's poll_remote_clients, decoding straight into the InputQueue (one
+ * launch does decode and tick; the deliveries never pass through
+ * remote_upto / remote_inputs).  Device pointers, stream ordered:
+ *   packets       tick t, remote handle h, session s: the packet at
+ *                 packets + ((t*num_players + h)*S + s)*packet_stride;
+ *                 packet_stride a multiple of 16, at least 32; the packet's
+ *                 length and start frame at lengths / start_frames[(t*num_players + h)*S + s]
+ *                 (length 0: none; entries of local handles ignored)
+ *   decode_status NULL, or int32 [num_players][S]: the last tick's result per
+ *                 endpoint (the codes of rb_decode_input_packets)
+ *   acks          NULL, or int32 [num_players][S]: after the call, the newest
+ *                 frame received per endpoint (RB_NULL_FRAME: none), the ack
+ *                 the receiver returns to the sender
+ * A malformed packet panics its session (the reference's decode().expect,
+ * "decoding failed"); a packet that skips frames never received is dropped
+ * (status -2).  Sparse saving, the fan-out, desync detection and peers'
+ * connect-status reports: RB_INVALID_REQUEST. */
+rb_status rb_p2p_run_ticks_packets(rb_p2p* b, int32_t n_ticks, const void* local_inputs, int64_t local_stride_bytes,
+                                   const uint8_t* packets, int64_t packet_stride, const int32_t* lengths,
+                                   const int32_t* start_frames, int32_t* decode_status, int32_t* acks);
+
 /* P2PSession::disconnect_player(handle) (p2p_session.rs:430-456, 555-581) in
  * every session whose `session_mask` byte is non-zero (NULL: all sessions),
  * called between rb_p2p_run_ticks calls (stream ordered).  Errors as the

@@ -214,3 +214,125 @@ def test_gpu_p2p_fed_through_the_wire_equals_direct_delivery(gpu_available, P, m
     for x, y in zip(wired.read_cells(), direct.read_cells()):
         np.testing.assert_array_equal(x, y)
     assert wired.totals()[2] > 0  # rollbacks happened on the wire-fed batch too
+
+
+def _encode_schedule(lib, P, S, T, mask, rd, upto, dr, stride, seed):
+    """Every tick's packets, encoded on the device ahead of the ticks: remote
+    handle h sends frames acked+1 .. upto[t, h], acked = the frame it knows
+    the receiver had one tick earlier minus 0-2 re-sent frames (an un-acked
+    sender); [T, P, S, stride] packets and [T, P, S] lengths / start frames."""
+    import ctypes
+
+    import torch
+    rng = np.random.default_rng(seed)
+    F = dr.shape[0]
+    pk = torch.zeros((T, P, S, stride), dtype=torch.uint8, device="cuda")
+    ln = torch.zeros((T, P, S), dtype=torch.int32, device="cuda")
+    st = torch.zeros((T, P, S), dtype=torch.int32, device="cuda")
+    du = torch.from_numpy(upto).cuda()
+    p = lambda t: ctypes.c_void_p(t.data_ptr())
+    for t in range(T):
+        for h in range(P):
+            if (mask >> h) & 1:
+                continue
+            prev = du[t - 1, h] if t > 0 else torch.full((S,), -1, dtype=torch.int32, device="cuda")
+            redo = torch.from_numpy(rng.integers(0, 3, S).astype(np.int32)).cuda()
+            acked = torch.where(prev < 0, prev, torch.clamp(prev - redo, min=rd - 1))
+            acked = torch.where(acked < rd, torch.full_like(acked, -1), acked).contiguous()
+            newest = du[t, h].contiguous()
+            assert lib.rb_encode_input_packets(0, None, h, P, S, 1, p(dr), F, rd, p(acked), p(newest), p(pk[t, h]),
+                                               stride, p(ln[t, h]), p(st[t, h])) == 0
+    torch.cuda.synchronize()
+    assert int((ln < 0).sum()) == 0
+    return pk, ln, st
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P,mask,rd,chunks", [(2, 0b01, 2, (1, 7, 30, 58)), (4, 0b0001, 1, (3, 1, 26, 66)),
+                                              (3, 0b010, 0, (96,))])
+def test_gpu_packet_ticks_equal_direct_delivery(gpu_available, P, mask, rd, chunks):
+    # rb_p2p_run_ticks_packets decodes every endpoint's packet inside the tick's
+    # poll (UdpProtocol::on_input fused into poll_remote_clients): fed the
+    # packets of a delivery schedule (with re-sent frames), the batch ends
+    # exactly where a batch fed the same deliveries directly does — cells,
+    # states, and the acks equal the schedule's newest delivered frames —
+    # over one-tick launches, HBM-cell multi-tick launches and LDS-ring ones.
+    import torch
+
+    import ggrs_amd as G
+    from ggrs_amd import _lib as L
+    from ggrs_amd.p2p import PlayerType, synth_network
+    lib = L.load()
+    S, W, T, stride = 512, 8, 96, 32
+    inputs, upto, rin = synth_network(S, P, T, mask, rd, 1, 5)
+
+    def batch():
+        b = (G.SessionBuilder(G.Game.EX_GAME, num_sessions=S).with_num_players(P).with_max_prediction_window(W)
+             .with_input_delay(1).with_remote_input_delay(rd))
+        for hh in range(P):
+            b.add_player(PlayerType.Local if (mask >> hh) & 1 else PlayerType.Remote, hh)
+        return b.start_p2p_session()
+
+    direct, wired = batch(), batch()
+    di, du, dr = (torch.from_numpy(a).cuda() for a in (inputs, upto, rin))
+    pk, ln, st = _encode_schedule(lib, P, S, T, mask, rd, upto, dr, stride, seed=5 + P)
+    dstat = torch.zeros((P, S), dtype=torch.int32, device="cuda")
+    acks = torch.full((P, S), -1, dtype=torch.int32, device="cuda")
+    direct.run_ticks(di, du, dr)
+    t = 0
+    for n in chunks:
+        wired.run_ticks_packets(di[t:t + n], pk[t:t + n], ln[t:t + n], st[t:t + n], dstat, acks)
+        t += n
+        torch.cuda.synchronize()
+        assert int((dstat < 0).sum()) == 0
+    assert t == T
+    remotes = [hh for hh in range(P) if not (mask >> hh) & 1]
+    np.testing.assert_array_equal(acks.cpu().numpy()[remotes], upto[-1][remotes])
+    np.testing.assert_array_equal(wired.read_live(), direct.read_live())
+    for x, y in zip(wired.read_cells(), direct.read_cells()):
+        np.testing.assert_array_equal(x, y)
+    np.testing.assert_array_equal(wired.read_queues(), direct.read_queues())
+    assert wired.totals()[2] > 0 and wired.counters()[2] == 0
+
+
+@pytest.mark.gpu
+def test_gpu_malformed_packet_panics_only_its_session(gpu_available):
+    # A packet the decoder cannot parse panics its session (the reference's
+    # decode(...).expect("decoding failed"), protocol.rs:656); a packet that
+    # skips frames never received is dropped (:639-642).  Every other session
+    # runs on as if fed directly.
+    import torch
+
+    import ggrs_amd as G
+    from ggrs_amd import _lib as L
+    from ggrs_amd.p2p import PlayerType, synth_network
+    lib = L.load()
+    S, P, W, T, stride, mask, rd = 256, 2, 8, 40, 32, 0b01, 1
+    inputs, upto, rin = synth_network(S, P, T, mask, rd, 1, 4)
+
+    def batch():
+        b = (G.SessionBuilder(G.Game.EX_GAME, num_sessions=S).with_num_players(P).with_max_prediction_window(W)
+             .with_input_delay(1).with_remote_input_delay(rd))
+        b.add_player(PlayerType.Local, 0)
+        b.add_player(PlayerType.Remote, 1)
+        return b.start_p2p_session()
+
+    direct, wired = batch(), batch()
+    di, du, dr = (torch.from_numpy(a).cuda() for a in (inputs, upto, rin))
+    pk, ln, st = _encode_schedule(lib, P, S, T, mask, rd, upto, dr, stride, seed=9)
+    bad_s, bad_t = 17, 20
+    k = int(ln[bad_t, 1, bad_s])
+    assert k > 0
+    pk[bad_t, 1, bad_s, k - 1] |= 0x80  # the last byte now continues a varint: truncated
+    dstat = torch.zeros((P, S), dtype=torch.int32, device="cuda")
+    direct.run_ticks(di, du, dr)
+    wired.run_ticks_packets(di[:bad_t], pk[:bad_t], ln[:bad_t], st[:bad_t], dstat)
+    wired.run_ticks_packets(di[bad_t:bad_t + 1], pk[bad_t:bad_t + 1], ln[bad_t:bad_t + 1], st[bad_t:bad_t + 1], dstat)
+    assert int(dstat[1, bad_s]) == -1
+    wired.run_ticks_packets(di[bad_t + 1:], pk[bad_t + 1:], ln[bad_t + 1:], st[bad_t + 1:], dstat)
+    status = wired.status()[0]
+    assert status[bad_s] == 101 and wired.counters()[2] == 1
+    ok = np.arange(S) != bad_s
+    np.testing.assert_array_equal(wired.read_live()[ok], direct.read_live()[ok])
+    with pytest.raises(G.InvalidRequest):  # packets need 16-byte rows of at least 32 bytes
+        wired.run_ticks_packets(di[:1], pk[:1, :, :, :16], ln[:1], st[:1])

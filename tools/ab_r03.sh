@@ -10,6 +10,8 @@ for rep in ${REPS:-1 2}; do
       p2p) args="--session p2p --steps 400 --warmup 32" ;;
       c4) args="--session p2p --num-players 4 --fanout --steps 100 --warmup 16" ;;
       wire) args="--session p2p --wire --steps 200 --warmup 32" ;;
+      p2p1) args="--session p2p --ticks-per-launch 1 --steps 200 --warmup 32" ;;
+      c4k8) args="--session p2p --num-players 4 --fanout --fanout-k 8 --steps 100 --warmup 16" ;;
       brawler1) args="--game brawler --ticks-per-launch 1 --steps 32 --warmup 8 --realtime-ticks 0" ;;
     esac
     for v in ${VARS:-base cur}; do

@@ -8,7 +8,7 @@ set -e
 cd "$(dirname "$0")/../ggrs_amd/csrc"
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -DRB_EXPERIMENTS=0"
 name=$1; shift
-mkdir -p build/var
+mkdir -p build/var ../var
 P2ONLY="-DRB_EXGAME_P2_ONLY=1"; [ -n "$ALLP" ] && P2ONLY=""
 /opt/rocm/bin/hipcc $F "$@" $P2ONLY -c -o build/var/ex_$name.o ops_exgame.hip
 OBJS=$(ls build/*.o | grep -v ops_exgame.o)
