@@ -19,7 +19,7 @@ export TMPDIR=/tmp
 EXTRA=${EXTRA:-}
 WARMUP=${WARMUP:-50}
 STEPS=${STEPS:-400}
-BENCH="bench.py --steps $STEPS --warmup $WARMUP --ticks-per-launch 50 --no-cpu-baseline $EXTRA"
+BENCH="bench.py --steps $STEPS --warmup $WARMUP --ticks-per-launch 50 --realtime-ticks 0 --no-cpu-baseline $EXTRA"
 run() {  # run <name> <timeout> <rocprof args...>
   local name=$1 t=$2; shift 2
   echo "=== $NAME/$name ($(date +%T))"
