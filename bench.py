@@ -741,9 +741,17 @@ def main():
         frames_per_tick = cd + 1
         total = S * world * frames_per_tick * args.steps
         value = total / elapsed
-        assert timed_ticks == args.steps, (timed_ticks, args.steps)
-        avg_kernel_s = kernel_ms / 1e3 / max(1, launches)  # per steady_kernel launch
-        ticks_per_launch = timed_ticks / max(1, launches)
+        # fused steady ticks exist for check distances 1..16 (kernels.hpp kMaxFusedCD); past that
+        # every tick is a tick_kernel launch, timed by events on every 8th one (engine sampling)
+        fused = 1 <= cd <= 16
+        if fused:
+            assert timed_ticks == args.steps, (timed_ticks, args.steps)
+            avg_kernel_s = kernel_ms / 1e3 / max(1, launches)  # per steady_kernel launch
+            ticks_per_launch = timed_ticks / max(1, launches)
+        else:
+            launches = timed_ticks  # the sampled launches
+            avg_kernel_s = kernel_ms / 1e3 / max(1, timed_ticks)
+            ticks_per_launch = 1
         # device words of one session's state: ex_game 5 f32 per player (frame
         # word implicit); brawler 256 entities x 8 i32
         nw = 256 * 8 if brawler else 5 * P
@@ -765,9 +773,11 @@ def main():
         cfg_key = f"{args.game} P={P} cd={cd} W={args.max_prediction} d={args.input_delay} S={S}" + (
             f" tpl={tpl}" if tpl != 50 else "")
         roofline = roofline_block(bytes_per_launch, avg_kernel_s, ticks_per_launch, launches,
-                                  (f"steady_kernel<Brawler<{P}>,{cd}>" if brawler else
-                                   f"steady_kernel<ExGame<{P},true>,{cd}>") +
-                                  (" (fused steady-state ticks)" if tpl > 1 else " (one tick per launch)"),
+                                  ((f"steady_kernel<Brawler<{P}>,{cd}>" if brawler else
+                                    f"steady_kernel<ExGame<{P},true>,{cd}>") +
+                                   (" (fused steady-state ticks)" if tpl > 1 else " (one tick per launch)"))
+                                  if fused else (f"tick_kernel<{'Brawler' if brawler else 'ExGame'}<{P}>> (one launch "
+                                                 f"per tick: no fused kernel past check distance 16)"),
                                   pmc_profile(cfg_key), model)
         roofline["algorithmic_bytes_per_session_tick"] = bpt
         roofline["measured_copy_GBps"] = measured_copy_gbps(dev)

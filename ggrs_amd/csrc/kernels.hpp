@@ -672,7 +672,8 @@ struct GameOps {
   virtual hipError_t launch_tick(const KParams& p, int block, hipStream_t st) const = 0;
   // fused steady-state ticks; hipErrorNotSupported when CD has no instantiation
   virtual hipError_t launch_steady(const RunParams& p, int cd, int block, hipStream_t st) const = 0;
-  bool launch_steady_supported(int cd) const { return cd >= 1 && cd <= 8; }
+  static constexpr int kMaxFusedCD = 16;  // steady_kernel instantiations: check distances 1..16
+  bool launch_steady_supported(int cd) const { return cd >= 1 && cd <= kMaxFusedCD; }
   virtual hipError_t launch_report(const void* cs, const int32_t* err, int S, int32_t frame, void* out,
                                    hipStream_t st) const = 0;
   // P2PSession ticks and the speculative fan-out (p2p.hpp); fan-out needs one
@@ -723,7 +724,7 @@ struct GameOpsT final : GameOps {
       return hipErrorNotSupported;  // experiment knobs need a RB_EXPERIMENTS=1 build
 #endif
     }
-    if constexpr (G::kHasPrep && HasFast<G>::value && CD >= 3 && CD % 2 == 1) {
+    if constexpr (G::kHasPrep && HasFast<G>::value && CD >= 3 && CD <= 7 && CD % 2 == 1) {  // (an A/B variant)
       if (p.pipe) {
         hipLaunchKernelGGL((steady_pipe_kernel<G, CD>), dim3(grid), dim3(block), 0, st, p);
         return hipGetLastError();
@@ -742,6 +743,14 @@ struct GameOpsT final : GameOps {
       case 6: return steady_cd<6>(p, block, st);
       case 7: return steady_cd<7>(p, block, st);
       case 8: return steady_cd<8>(p, block, st);
+      case 9: return steady_cd<9>(p, block, st);
+      case 10: return steady_cd<10>(p, block, st);
+      case 11: return steady_cd<11>(p, block, st);
+      case 12: return steady_cd<12>(p, block, st);
+      case 13: return steady_cd<13>(p, block, st);
+      case 14: return steady_cd<14>(p, block, st);
+      case 15: return steady_cd<15>(p, block, st);
+      case 16: return steady_cd<16>(p, block, st);
       default: return hipErrorNotSupported;
     }
   }

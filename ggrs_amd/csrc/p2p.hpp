@@ -687,8 +687,12 @@ constexpr int kFanGroup = 4;  // branches a lane advances together (its independ
 // operations run in the reference's order, except that the tick's final
 // SaveGameState moves behind set_last_confirmed_frame and add_local_input,
 // which touch neither the state nor the cells.
+#ifndef RB_P2P_WAVES_PER_EU
+#define RB_P2P_WAVES_PER_EU 1  // >1: ask the compiler for that many waves per SIMD (VGPR cap; A/B builds)
+#endif
 template <class G, bool kSpec, bool kSparse, bool kNet, bool kLdsC, bool kAsync, bool kWire = false>
-__global__ void __launch_bounds__(256) p2p_kernel(const P2PParams p) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RB_P2P_WAVES_PER_EU)))
+p2p_kernel(const P2PParams p) {
   static_assert(!kAsync || (kLdsC && !kSpec && !kNet), "lane-asynchronous ticks: plain or sparse path, LDS cells");
   static_assert(!kWire || (!kSpec && !kSparse && !kNet && !kAsync), "packet-fed ticks: the plain lock-step path");
   using InRec = typename G::InRec;

@@ -417,13 +417,16 @@ def test_config5_shard_131072_sessions_with_audit_replicas(gpu_available):
                                            (G.Game.EX_GAME, 1, 8, 4, 0), (G.Game.EX_GAME, 3, 6, 5, 1),
                                            (G.Game.EX_GAME, 4, 9, 8, 3), (G.Game.EX_GAME, 2, 12, 11, 2),
                                            (G.Game.STUB, 2, 8, 7, 2), (G.Game.STUB, 2, 8, 2, 0),
-                                           (G.Game.STUB_ENUM, 2, 8, 3, 1), (G.Game.EX_GAME, 2, 4, 3, 0)])
+                                           (G.Game.STUB_ENUM, 2, 8, 3, 1), (G.Game.EX_GAME, 2, 4, 3, 0),
+                                           (G.Game.EX_GAME, 2, 17, 16, 1), (G.Game.STUB, 2, 16, 13, 0),
+                                           (G.Game.EX_GAME, 2, 24, 20, 0)])
 @pytest.mark.parametrize("pipe", [True, False], ids=["pipe", "onetick"])
 def test_run_ticks_fused_parity(gpu_available, monkeypatch, game, P, W, cd, d, pipe):
     """rb_run_ticks fuses consecutive steady-state ticks into one launch
-    (steady_kernel<G, CD>, CD <= 8; larger cd falls back to per-tick launches;
-    ex_game at odd CD >= 3 runs two ticks in flight, steady_pipe_kernel, unless
-    RB_STEADY_PIPE=0).  Chunks of ticks are compared bit-exactly with the oracle."""
+    (steady_kernel<G, CD>, CD <= 16; larger cd falls back to per-tick launches,
+    the cd 20 case; with RB_STEADY_PIPE=1 ex_game at odd 3 <= CD <= 7 runs two
+    ticks in flight, steady_pipe_kernel).  Chunks of ticks are compared
+    bit-exactly with the oracle."""
     import torch
     monkeypatch.setenv("RB_STEADY_PIPE", "1" if pipe else "0")
     S, T = 150, 120
