@@ -207,7 +207,8 @@ def roofline_block(bytes_per_launch, avg_kernel_s, ticks_per_launch, launches, k
     bytes the counters saw (`traffic`) and their fraction of peak (`dram_frac`),
     the VALU issue-slot fraction, and `bound` = what actually limits the
     kernel, decided from those counters: "hbm" when the DRAM-side traffic is
-    above 0.7 of peak, "valu" when the VALU issue slots are above 0.7 busy,
+    above 0.7 of the measured store ceiling (what DRAM takes in practice,
+    profiles/r02_calib_write.json), "valu" when the VALU issue slots are above 0.7 busy,
     "latency" (dependent chains at low occupancy) otherwise; "unprofiled"
     when no PMC profile of this configuration is committed."""
     achieved = bytes_per_launch / avg_kernel_s / 1e9
@@ -226,8 +227,12 @@ def roofline_block(bytes_per_launch, avg_kernel_s, ticks_per_launch, launches, k
             r["valu"] = {k: iss[k] for k in ("valu_insts_per_wave", "valu_issue_frac", "issue_stall_frac",
                                               "waves_per_simd", "waves_dispatched_per_simd", "clock_GHz_sq",
                                               "l2_hit") if k in iss}
-            if r["dram_frac"] > 0.7:
-                r["bound"], r["limiter"] = "hbm", "hbm bandwidth"
+            # against what DRAM delivers in practice: the calibrated store ceiling (5.9 TB/s), not the spec
+            ceil = store_ceiling_gbps() or HBM_PEAK_GBS
+            r["dram_frac_of_ceiling"] = traffic / avg_kernel_s / 1e9 / ceil
+            if r["dram_frac_of_ceiling"] > 0.7:
+                r["bound"], r["limiter"] = "hbm", (f"hbm bandwidth: {r['dram_frac_of_ceiling']:.2f} of the "
+                                                   f"{ceil:.0f} GB/s measured store ceiling")
             elif iss["valu_issue_frac"] > 0.7:
                 r["bound"], r["limiter"] = "valu", "valu issue"
             else:
@@ -376,8 +381,49 @@ def bench_p2p(args):
         tick_args = [(sess._h, 1, ptr(di[t]), lstride, ptr(pk), stride, ptr(ln), ptr(st), None, ptr(acks))
                      for t in range(T)]
         enc, tick_fn = lib.rb_encode_input_packets, lib.rb_p2p_run_ticks_packets
+    if args.wire_replay:  # received traffic replayed: every tick's packets encoded ahead (untimed)
+        import ctypes
+        lib = G._lib.load()
+        F = dr.shape[0]
+        stride = 32
+        pk = torch.zeros((T, P, S, stride), dtype=torch.uint8, device=dev)
+        ln, st = (torch.zeros((T, P, S), dtype=torch.int32, device=dev) for _ in range(2))
+        ptr = lambda t: ctypes.c_void_p(t.data_ptr())
+        sp = ctypes.c_void_p(stream.cuda_stream)
+        rng = np.random.default_rng(args.seed)
+        with torch.cuda.stream(stream):
+            none = torch.full((S,), -1, dtype=torch.int32, device=dev)
+            for t in range(T):
+                for h in range(P):
+                    if (mask >> h) & 1:
+                        continue
+                    # the peer knows the receiver had the previous tick's deliveries and re-sends 0-2
+                    # frames before them (an un-acked sender), as tests/test_wire.py's schedule
+                    prev = du[t - 1, h] if t > 0 else none
+                    redo = torch.from_numpy(rng.integers(0, 3, S).astype(np.int32)).to(dev)
+                    acked = torch.where(prev < 0, prev, torch.clamp(prev - redo, min=args.remote_delay - 1))
+                    acked = torch.where(acked < args.remote_delay, none, acked).contiguous()
+                    assert lib.rb_encode_input_packets(local, sp, h, P, S, 1, ptr(dr), F, args.remote_delay,
+                                                       ptr(acked), ptr(du[t, h].contiguous()), ptr(pk[t, h]), stride,
+                                                       ptr(ln[t, h]), ptr(st[t, h])) == 0
+            torch.cuda.synchronize()
+        assert int((ln < 0).sum()) == 0, "a packet did not fit its row"
+        lstride = P * S * di.element_size()
+        replay_args = [(sess._h, min(T, t + tpl) - t, ptr(di[t]), lstride, ptr(pk[t]), stride, ptr(ln[t]), ptr(st[t]),
+                        None, None) for t in range(T)]
+        tick_fn = lib.rb_p2p_run_ticks_packets
 
     def run(t0, t1):
+        if args.wire_replay:
+            bad = 0
+            for t in range(t0, t1, tpl):
+                a = replay_args[t]
+                if a[1] != min(t1, t + tpl) - t:
+                    a = (a[0], min(t1, t + tpl) - t) + a[2:]
+                bad |= tick_fn(*a)
+            if bad:
+                raise SystemExit("wire replay: a call failed")
+            return
         if not args.wire:
             for t in range(t0, t1, tpl):
                 e = min(t1, t + tpl)
@@ -440,7 +486,7 @@ def bench_p2p(args):
         avg_kernel_s = kernel_ms / 1e3 / max(1, launches)
         cfg_key = (f"p2p {args.game} P={P} W={W} d={args.input_delay} rd={args.remote_delay} lag={lo},{hi} S={S}"
                    + (" sparse" if args.sparse_saving else "") + (f" fanout{'' if K == 16 else K}" if args.fanout else "")
-                   + (" wire" if args.wire else ""))
+                   + (" wire" if args.wire else "") + (" wire-replay" if args.wire_replay else ""))
         gname = f"Brawler<{P}>" if brawler else f"ExGame<{P},true>"
         roofline = roofline_block(bytes_rank / max(1, launches), avg_kernel_s, args.steps / max(1, launches), launches,
                                   f"p2p_kernel<{gname}>" + ((" + fanout_kernel (per tick)" if generic_fan or brawler
@@ -460,7 +506,10 @@ def bench_p2p(args):
                                    + (f", speculative fan-out {K} candidates/frame" if args.fanout else "")
                                    + f", inputs masked 0x{imask:X}"
                                    + (", inputs delivered as packets (per tick: the peers' device encode, then "
-                                      "one launch decoding them inside the tick)" if args.wire else ""),
+                                      "one launch decoding them inside the tick)" if args.wire else "")
+                                   + (f", inputs delivered as packets: received traffic replayed ({tpl} ticks per "
+                                      "launch, each decoding its packets inside the tick; the peers' packets encoded "
+                                      "before the timed region)" if args.wire_replay else ""),
                        "sessions_per_gpu": S, "total_sessions": S * world,
                        "advance_frames_per_session_tick": adv / (S * world * args.steps),
                        "rollbacks_per_session_tick": (loads + selects) / (S * world * args.steps),
@@ -533,6 +582,9 @@ def main():
     ap.add_argument("--wire", action="store_true",
                     help="p2p: remote inputs travel as packets each tick: device encode (send_pending_output) + "
                          "decode (on_input) into the delivery tensors, then one P2P tick")
+    ap.add_argument("--wire-replay", action="store_true",
+                    help="p2p: the remote inputs arrive as the peers' packets, recorded ahead (untimed) and replayed "
+                         "--ticks-per-launch ticks per launch, each tick decoding its packets (rb_p2p_run_ticks_packets)")
     ap.add_argument("--fanout", action="store_true",
                     help="p2p: speculative fan-out, --fanout-k candidate inputs per session per tick (BASELINE "
                          "configs[3]; use with --num-players 4)")

@@ -30,4 +30,5 @@ b p2p 600 --session p2p --steps 400 --warmup 32 &&
 b p2p_sparse 600 --session p2p --sparse-saving --steps 400 --warmup 32 &&
 b c4 600 --session p2p --num-players 4 --fanout --steps 100 --warmup 16 &&
 b c4_k8 600 --session p2p --num-players 4 --fanout --fanout-k 8 --steps 100 --warmup 16 --no-cpu-baseline &&
-b wire 600 --session p2p --wire --steps 200 --warmup 32
+b wire 600 --session p2p --wire --steps 200 --warmup 32 &&
+b wire_replay 600 --session p2p --wire-replay --steps 400 --warmup 32
