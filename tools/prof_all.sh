@@ -20,3 +20,4 @@ NAME=p2p EXTRA="--session p2p" bash tools/prof_round.sh || exit $?
 NAME=p2p_sparse EXTRA="--session p2p --sparse-saving" bash tools/prof_round.sh || exit $?
 NAME=c4 EXTRA="--session p2p --num-players 4 --fanout" STEPS=100 WARMUP=16 bash tools/prof_round.sh || exit $?
 NAME=wire EXTRA="--session p2p --wire" STEPS=200 WARMUP=16 bash tools/prof_round.sh || exit $?
+NAME=wire_replay EXTRA="--session p2p --wire-replay" STEPS=400 WARMUP=50 bash tools/prof_round.sh || exit $?
