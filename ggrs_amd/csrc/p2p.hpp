@@ -1198,6 +1198,42 @@ p2p_kernel(const P2PParams p) {
       if (last != kNullFrame && last + 1 < start) return kWireGap;
       if (last != kNullFrame && (start - 1 < last - 2 * W || start - 1 < kNullFrame)) return kWireNothing;
       const uint32_t ref = (last != kNullFrame && start - 1 != kNullFrame) ? ring.get(start - 1, h, s) : 0u;
+      // The two packet shapes a tick's delta of a few inputs takes: one literal run of every byte, or
+      // (inputs equal to the reference) one compressed run.  Both are valid by their header alone, so
+      // their inputs are added in one pass, without the general parse below.
+      {
+        const uint32_t h0 = w0[0] & 0xFFu;
+        const bool lit = !(h0 & 0x81u) && static_cast<int32_t>(h0 >> 1) == n - 1 && n <= 32 && (n - 1) % IB == 0;
+        const bool run = (h0 & 0x81u) == 1u && n == 1 && (h0 >> 2) % IB == 0;
+        if (lit || run) {
+          const int32_t nb = lit ? n - 1 : static_cast<int32_t>(h0 >> 2);
+          const uint32_t fill = (h0 & 2u) ? 0xFFu : 0u;
+          uint32_t win[8];
+#pragma unroll
+          for (int i = 0; i < 7; ++i) win[i] = __builtin_amdgcn_alignbyte(w0[i + 1], w0[i], 1);  // skip the header
+          win[7] = w0[7] >> 8;
+          uint32_t acc = 0;
+          for (int32_t k = 0; k < nb; ++k) {
+            const uint32_t x = lit ? (win[0] & 0xFFu) : fill;
+            if (lit) {
+#pragma unroll
+              for (int i = 0; i < 7; ++i) win[i] = __builtin_amdgcn_alignbyte(win[i + 1], win[i], 1);
+              win[7] >>= 8;
+            }
+            const int i = k % IB;
+            acc |= (((ref >> (8 * i)) ^ x) & 0xFFu) << (8 * i);
+            if (i == IB - 1) {
+              const int32_t f = start + k / IB;
+              if (f > last) {  // protocol.rs:661-663
+                q_add(q[j], ring, h, s, f, acc);
+                q[j].conn_last = f;
+              }
+              acc = 0;
+            }
+          }
+          return start + nb / IB - 1 > last ? kWireOk : kWireNothing;
+        }
+      }
       // pass 0 validates (and counts the bytes the inputs take), pass 1 adds the inputs
       int32_t nbytes = 0;
       for (int pass = 0; pass < 2; ++pass) {
