@@ -1,6 +1,6 @@
 // ggrs_amd/csrc/engine.hip — MI355X batched rollback-resimulation engine: host side
 // (rb_batch, the C ABI of include/ggrs_amd.h).  Kernels: kernels.hpp, instantiated
-// per game in ops_exgame.hip / ops_brawler.hip / ops_stub.hip.
+// per game in ops_exgame.hip / ops_exgame_lps.hip / ops_brawler.hip / ops_stub.hip.
 //
 //
 // One rb_batch = S independent SyncTestSessions in lock-step.  Per tick the
