@@ -256,8 +256,11 @@ typedef struct rb_p2p_config {
  * is candidate 0), then the smallest values not taken.  A later misprediction
  * of that handle alone, held at one candidate value, becomes a branch select
  * instead of LoadGameState + resimulation; cells, states, statuses and frames
- * stay identical to the plain rollback.  ex_game (one lane per player) and the
- * brawler (one wave per session); not with sparse saving. */
+ * stay identical to the plain rollback.  Candidates that act alike on the
+ * player share one branch (ex_game's 16 inputs are 9 trajectories).  ex_game
+ * (one lane per player: the fan-out runs inside the P2P tick, so a call of many
+ * ticks is one launch) and the brawler (one wave per session: a fan-out launch
+ * between one-tick P2P launches); not with sparse saving. */
 #define RB_P2P_FLAG_FANOUT 4u
 
 /* Peers' connect-status reports (update_player_disconnects, p2p_session.rs:707-742):
