@@ -654,6 +654,9 @@ constexpr bool inlane_fan() {
   else return false;
 }
 constexpr int kFanGroup = 4;  // branches a lane advances together (its independent chains)
+#ifndef RB_FAN_ROT
+#define RB_FAN_ROT 0  // 1: branch k in lane (k + speculated handle) % L (A/B builds; measured no better)
+#endif
 #ifndef RB_FAN_INRANGE
 #define RB_FAN_INRANGE 1  // 0: the fan-out's chains always take the general AdvanceFrame (A/B builds)
 #endif
@@ -982,7 +985,7 @@ p2p_kernel(const P2PParams p) {
       // players' fletcher parts
       if constexpr (kInFan) {
         const unsigned Gs = Spad * static_cast<unsigned>(kSpecBranches + L);
-        const int owner = kk % L;
+        const int owner = RB_FAN_ROT ? (kk + rs) % L : kk % L;  // (fan_inlane's branch-to-lane map)
         const unsigned col = s * kSpecBranches + static_cast<unsigned>(kk);
         const unsigned ocol = Spad * kSpecBranches + s * L + static_cast<unsigned>(lane);  // this lane's player, once
         const bool other = lane < P && lane != rs;
@@ -1574,6 +1577,7 @@ p2p_kernel(const P2PParams p) {
       const unsigned Gs = Spad * static_cast<unsigned>(kSpecBranches + L);  // branch columns, then the others'
       const unsigned ocol = Spad * kSpecBranches + s * L + static_cast<unsigned>(lane);
       constexpr int kB = kSpecBranches / L;  // branches per lane
+      const int krot = RB_FAN_ROT ? (lane - rs + L) % L : lane;  // branch k runs in lane k % L (RB_FAN_ROT: (k + rs) % L)
       // every chain of the wave starts in range (games.hpp in_range: e.g. ex_game rotations in [+0, 6.5),
       // which stay there for any number of frames): the AdvanceFrames skip the out-of-range library paths
       bool inr = false;
@@ -1594,7 +1598,7 @@ p2p_kernel(const P2PParams p) {
         bool on[kFanGroup];
 #pragma unroll
         for (int b = 0; b < kFanGroup; ++b) {
-          const int k = (b0 + b) * L + lane;
+          const int k = (b0 + b) * L + krot;
           on[b] = k < nb;
           in[b] = static_cast<InRec>(static_cast<uint64_t>(cand_at(cand, k)) << (8 * rs));
 #pragma unroll
@@ -1608,7 +1612,7 @@ p2p_kernel(const P2PParams p) {
             for (int b = 0; b < kFanGroup; ++b)
               if (on[b])
                 store_words<NW>(p.spec_cells + slot * NW * Gs, static_cast<int>(Gs),
-                                static_cast<int>(s * kSpecBranches + static_cast<unsigned>((b0 + b) * L + lane)), wb[b]);
+                                static_cast<int>(s * kSpecBranches + static_cast<unsigned>((b0 + b) * L + krot)), wb[b]);
             if (run_own) store_words<NW>(p.spec_cells + slot * NW * Gs, static_cast<int>(Gs), static_cast<int>(ocol), ow);
           }
 #pragma unroll
@@ -1627,7 +1631,7 @@ p2p_kernel(const P2PParams p) {
         for (int b = 0; b < kFanGroup; ++b)
           if (on[b])
             store_words<NW>(p.spec_state, static_cast<int>(Gs),
-                            static_cast<int>(s * kSpecBranches + static_cast<unsigned>((b0 + b) * L + lane)), wb[b]);
+                            static_cast<int>(s * kSpecBranches + static_cast<unsigned>((b0 + b) * L + krot)), wb[b]);
       }
       tot_branch += static_cast<uint32_t>(cur - base) * static_cast<uint32_t>(nb);
     }
