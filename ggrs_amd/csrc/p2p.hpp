@@ -903,7 +903,11 @@ p2p_kernel(const P2PParams p) {
   auto adjust_begin = [&](int32_t first_incorrect) __attribute__((always_inline)) -> int32_t {
     const int32_t to_load = kSparse ? last_saved : first_incorrect;
     const int32_t count = cur - to_load;
-    const unsigned slot = static_cast<unsigned>(to_load % W);
+    const unsigned slot = static_cast<unsigned>(max(to_load, 0) % W);
+    // (HBM cells: the cell's words are loaded with its tag, before the checks, so the
+    // LoadGameState costs one global round trip instead of two)
+    [[maybe_unused]] uint32_t cw[NW];
+    if constexpr (!kLdsC) load_words<NW>(p.snap + slot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), cw);
     const int32_t tag = kLdsC ? lds_tag[slot * bps + sl] : p.tag[slot * Spad + s];
     if (to_load < 0 || to_load > first_incorrect || count <= 0 || count > W || tag != to_load) {
       status = kP2PStatusPanic;  // a reference assert (sync_layer.rs:141-148) would fire
@@ -914,7 +918,8 @@ p2p_kernel(const P2PParams p) {
 #pragma unroll
         for (int n = 0; n < NW; ++n) w[n] = lds_cell[(slot * NW + n) * bd + tid];
       } else {
-        load_words<NW>(p.snap + slot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), w);
+#pragma unroll
+        for (int n = 0; n < NW; ++n) w[n] = cw[n];
       }
       ++tot_load;
     }
