@@ -301,7 +301,7 @@ rb_status rb_synctest_create(const rb_config* cfg, rb_batch** out) {
   if (cfg->input_delay > kQueueLen - cfg->max_prediction - 2)
     return fail(nullptr, RB_INVALID_REQUEST, "input delay does not fit the 128-entry input queue");
   auto ops = make_game(cfg->game, cfg->num_players, (cfg->flags & RB_FLAG_LANE_PER_SESSION) != 0);
-  if (!ops) return fail(nullptr, RB_INVALID_REQUEST, "unsupported game / num_players combination");
+  if (!ops) return fail(nullptr, RB_INVALID_REQUEST, "unsupported game / num_players combination (RB_FLAG_LANE_PER_SESSION: A/B builds only)");
   // every snapshot word offset (slot * NW * lanes * Spad + ...) is 32-bit inside the kernels
   if (static_cast<uint64_t>(cfg->max_prediction) * ops->nw * ops->lanes *
           ((static_cast<uint64_t>(cfg->num_sessions) + 63) / 64 * 64) >= (1ull << 32))
@@ -316,7 +316,9 @@ rb_status rb_synctest_create(const rb_config* cfg, rb_batch** out) {
   b->W = cfg->max_prediction;
   b->P = cfg->num_players;
   b->block = cfg->block_size ? static_cast<int>(cfg->block_size) : 256;
+#if RB_EXPERIMENTS  // steady_pipe_kernel exists in A/B builds only
   if (const char* env = std::getenv("RB_STEADY_PIPE")) b->pipe = std::atoi(env) != 0;
+#endif
   if (b->block % 64 != 0 || b->block > 256) return fail(nullptr, RB_INVALID_REQUEST, "block_size must be 64, 128, 192 or 256");
   b->plan_only = cfg->device < 0;
   b->device = cfg->device;

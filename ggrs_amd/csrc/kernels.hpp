@@ -162,32 +162,14 @@ template <class G, class Pr>
 __device__ __forceinline__ void advance_fast(uint32_t (&w)[G::NWL], const Pr& pr, int k, uint32_t& special) {
   if constexpr (HasFast<G>::value) G::advance_prepared_fast(w, pr, k, special);
 }
-#ifndef RB_FAST_ADVANCE
-#define RB_FAST_ADVANCE 0  // 1: the branch-free AdvanceFrame with redo (A/B builds, tools/mkvar.sh): measured
-                           // neutral on p2p_kernel (191 vs 191 us per 50 ticks, round 3)
-#endif
 // One AdvanceFrame{inputs} (State::advance, ex_game.rs:259-321) for the
-// kernels that run frames one at a time (tick_kernel, p2p_kernel, the
-// fan-out): a game with G::kHasFast runs its branch-free form, and the wave
-// redoes the frame in the general form from the same state when any active
-// lane flagged an operand the fast form does not cover.
+// kernels that run frames one at a time (tick_kernel, p2p_kernel, the fan-out).
+// (Round 3 measured a branch-free form with a wave-wide redo here: neutral on
+// p2p_kernel, so it was dropped.)
 template <class G>
 __device__ __forceinline__ void advance_frame(uint32_t (&w)[G::NWL], typename G::InRec in, int lane, uint32_t dmask,
                                               uint32_t* unexpected) {
-  if constexpr (HasFast<G>::value && RB_FAST_ADVANCE) {
-    uint32_t w0[G::NWL];
-#pragma unroll
-    for (int i = 0; i < G::NWL; ++i) w0[i] = w[i];
-    uint32_t special = 0;
-    G::advance_fast(w, in, lane, dmask, special);
-    if (__any(special != 0u)) {
-#pragma unroll
-      for (int i = 0; i < G::NWL; ++i) w[i] = w0[i];
-      G::advance(w, in, lane, dmask, unexpected);
-    }
-  } else {
-    G::advance(w, in, lane, dmask, unexpected);
-  }
+  G::advance(w, in, lane, dmask, unexpected);
 }
 // The fused tick.  Thread g serves lane (g % L) of session g / L; a session's
 // state slice stays in that lane's VGPRs for the whole tick.  Phase 1 issues
@@ -392,9 +374,12 @@ struct DecSel<G, true> {
 };
 template <class G>
 using DecOf = typename DecSel<G>::type;
-#ifndef RB_STEADY_FAST
-#define RB_STEADY_FAST 0  // 1: the branch-free form with the tick redo (A/B builds, tools/mkvar.sh): measured
-                          // slower, 269 vs 220 us per 50 ticks (round 3)
+// RB_STEADY_FAST (RB_EXPERIMENTS builds only): the branch-free form with the tick redo, measured
+// slower (269 vs 220 us per 50 ticks, round 3); never compiled into the product library.
+#if RB_EXPERIMENTS && defined(RB_STEADY_FAST_AB)
+#define RB_STEADY_FAST 1
+#else
+#define RB_STEADY_FAST 0
 #endif
 
 // kExp: attribution experiments (RunParams::debug knobs, tools/exp_steady.py);
@@ -640,7 +625,9 @@ __global__ void __launch_bounds__(256) steady_kernel(const RunParams p) {
 }
 
 }  // namespace rb
-#include "steady_pipe.hpp"  // two ticks in flight per lane (uses settle / HasFast above)
+#if RB_EXPERIMENTS
+#include "steady_pipe.hpp"  // two ticks in flight per lane (measured slower: A/B builds only)
+#endif
 namespace rb {
 
 template <class G>
@@ -724,12 +711,14 @@ struct GameOpsT final : GameOps {
       return hipErrorNotSupported;  // experiment knobs need a RB_EXPERIMENTS=1 build
 #endif
     }
+#if RB_EXPERIMENTS
     if constexpr (G::kHasPrep && HasFast<G>::value && CD >= 3 && CD <= 7 && CD % 2 == 1) {  // (an A/B variant)
       if (p.pipe) {
         hipLaunchKernelGGL((steady_pipe_kernel<G, CD>), dim3(grid), dim3(block), 0, st, p);
         return hipGetLastError();
       }
     }
+#endif
     hipLaunchKernelGGL((steady_kernel<G, CD, false>), dim3(grid), dim3(block), 0, st, p);
     return hipGetLastError();
   }

@@ -1,22 +1,31 @@
-// ggrs_amd/csrc/ops_exgame.hip — device code of examples/ex_game (kernels.hpp
-// instantiated for ExGame<P, lane-per-player>; the lane-per-session layout
-// builds in ops_exgame_lps.hip, a translation unit of its own so the two
-// compile in parallel).
+// ggrs_amd/csrc/ops_exgame.hip — device code of examples/ex_game: the factory.
+// Each player count instantiates kernels.hpp for ExGame<P, lane-per-player> in a
+// translation unit of its own (ops_exgame_p<P>.hip), so they compile in
+// parallel; the lane-per-session layout (ops_exgame_lps.hip) is an A/B build only.
 #include "kernels.hpp"
 
 namespace rb {
-std::unique_ptr<GameOps> make_exgame_lps_ops(int players);  // ops_exgame_lps.hip
+std::unique_ptr<GameOps> make_exgame_lps_ops(int players);  // ops_exgame_lps.hip (RB_EXPERIMENTS)
+std::unique_ptr<GameOps> make_exgame_p1_ops();
+std::unique_ptr<GameOps> make_exgame_p2_ops();
+std::unique_ptr<GameOps> make_exgame_p3_ops();
+std::unique_ptr<GameOps> make_exgame_p4_ops();
 std::unique_ptr<GameOps> make_exgame_ops(int players, bool lane_per_session) {
-#if RB_EXGAME_P2_ONLY  // kernel-experiment builds (tools/): the bench configuration only
-  if (players == 2 && !lane_per_session) return std::make_unique<GameOpsT<ExGame<2, true>>>();
-  return nullptr;
-#else
+  // the lane-per-session layout (measured slower: 5.35 vs 4.4 us per tick) is built into A/B
+  // builds only (RB_EXPERIMENTS=1); the product library refuses RB_FLAG_LANE_PER_SESSION
+#if RB_EXPERIMENTS
   if (lane_per_session) return make_exgame_lps_ops(players);
+#else
+  if (lane_per_session) return nullptr;
+#endif
+#if RB_EXGAME_P2_ONLY  // kernel-experiment builds (tools/): the bench configuration only
+  return players == 2 ? make_exgame_p2_ops() : nullptr;
+#else
   switch (players) {
-    case 1: return std::make_unique<GameOpsT<ExGame<1, true>>>();
-    case 2: return std::make_unique<GameOpsT<ExGame<2, true>>>();
-    case 3: return std::make_unique<GameOpsT<ExGame<3, true>>>();
-    case 4: return std::make_unique<GameOpsT<ExGame<4, true>>>();
+    case 1: return make_exgame_p1_ops();
+    case 2: return make_exgame_p2_ops();
+    case 3: return make_exgame_p3_ops();
+    case 4: return make_exgame_p4_ops();
     default: return nullptr;
   }
 #endif

@@ -59,7 +59,9 @@ constexpr int kQsFields = QS_PLAYER0 + QF_COUNT * 4;
 enum : int { TR_LOAD = 0, TR_NADV = 1, TR_NSAVE = 2, TR_COUNT = 3 };
 constexpr int32_t kP2PStatusOk = 0, kP2PStatusThreshold = 1, kP2PStatusPanic = 101;
 // decode status of a packet-fed tick's endpoint (the codes of wire.hip's rb_decode_input_packets):
-// inputs added, nothing new, malformed (the reference panics, protocol.rs:656), a gap (dropped, :639-642)
+// inputs added, nothing new, malformed (the reference panics, protocol.rs:656; also a length past
+// the packet row), a gap (a packet starting past the frame after the last one received: the
+// reference's assert!, protocol.rs:639-642, so inside a tick the session panics too)
 constexpr int32_t kWireOk = 0, kWireNothing = 1, kWirePanic = -1, kWireGap = -2;
 // executed work: AdvanceFrames, SaveGameStates, LoadGameStates, rollbacks
 // replaced by a speculative branch select, branch frames presimulated
@@ -654,9 +656,6 @@ constexpr bool inlane_fan() {
   else return false;
 }
 constexpr int kFanGroup = 4;  // branches a lane advances together (its independent chains)
-#ifndef RB_FAN_ROT
-#define RB_FAN_ROT 0  // 1: branch k in lane (k + speculated handle) % L (A/B builds; measured no better)
-#endif
 #ifndef RB_FAN_INRANGE
 #define RB_FAN_INRANGE 1  // 0: the fan-out's chains always take the general AdvanceFrame (A/B builds)
 #endif
@@ -990,7 +989,7 @@ p2p_kernel(const P2PParams p) {
       // players' fletcher parts
       if constexpr (kInFan) {
         const unsigned Gs = Spad * static_cast<unsigned>(kSpecBranches + L);
-        const int owner = RB_FAN_ROT ? (kk + rs) % L : kk % L;  // (fan_inlane's branch-to-lane map)
+        const int owner = kk % L;  // (fan_inlane's branch-to-lane map)
         const unsigned col = s * kSpecBranches + static_cast<unsigned>(kk);
         const unsigned ocol = Spad * kSpecBranches + s * L + static_cast<unsigned>(lane);  // this lane's player, once
         const bool other = lane < P && lane != rs;
@@ -1202,8 +1201,9 @@ p2p_kernel(const P2PParams p) {
         w0[0] = a.x, w0[1] = a.y, w0[2] = a.z, w0[3] = a.w, w0[4] = b.x, w0[5] = b.y, w0[6] = b.z, w0[7] = b.w;
       }
       if (q[j].disc || n <= 0) return kWireNothing;  // a disconnected player's endpoint no longer runs
+      if (n > p.packet_stride) return kWirePanic;    // the row does not hold that many bytes
       const int32_t last = q[j].conn_last;
-      if (last != kNullFrame && last + 1 < start) return kWireGap;
+      if (last != kNullFrame && last + 1 < start) return kWireGap;  // assert! (protocol.rs:639-642)
       if (last != kNullFrame && (start - 1 < last - 2 * W || start - 1 < kNullFrame)) return kWireNothing;
       const uint32_t ref = (last != kNullFrame && start - 1 != kNullFrame) ? ring.get(start - 1, h, s) : 0u;
       // The two packet shapes a tick's delta of a few inputs takes: one literal run of every byte, or
@@ -1354,7 +1354,8 @@ p2p_kernel(const P2PParams p) {
         if (h < P && !((p.local_mask >> h) & 1u)) {
           const int32_t ds = wire_poll(j, h, t);
           if (p.pk_status) p.pk_status[static_cast<size_t>(h) * p.S + s] = ds;
-          if (ds == kWirePanic) status = kP2PStatusPanic;  // the reference panics ("decoding failed")
+          // the reference panics: "decoding failed" (protocol.rs:656) or the gap assert (:639-642)
+          if (ds == kWirePanic || ds == kWireGap) status = kP2PStatusPanic;
         }
         continue;
       }
@@ -1582,7 +1583,7 @@ p2p_kernel(const P2PParams p) {
       const unsigned Gs = Spad * static_cast<unsigned>(kSpecBranches + L);  // branch columns, then the others'
       const unsigned ocol = Spad * kSpecBranches + s * L + static_cast<unsigned>(lane);
       constexpr int kB = kSpecBranches / L;  // branches per lane
-      const int krot = RB_FAN_ROT ? (lane - rs + L) % L : lane;  // branch k runs in lane k % L (RB_FAN_ROT: (k + rs) % L)
+      const int krot = lane;  // branch k runs in lane k % L
       // every chain of the wave starts in range (games.hpp in_range: e.g. ex_game rotations in [+0, 6.5),
       // which stay there for any number of frames): the AdvanceFrames skip the out-of-range library paths
       bool inr = false;

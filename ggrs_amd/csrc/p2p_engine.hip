@@ -213,7 +213,7 @@ rb_status rb_p2p_create(const rb_p2p_config* cfg, rb_p2p** out) {
     return pfail(nullptr, RB_INVALID_REQUEST,
                  "P2P batches support ex_game, the stub games, the brawler and registered plugin games");
   auto ops = make_game(cfg->game, cfg->num_players, (cfg->flags & RB_FLAG_LANE_PER_SESSION) != 0);
-  if (!ops) return pfail(nullptr, RB_INVALID_REQUEST, "unsupported game / num_players combination");
+  if (!ops) return pfail(nullptr, RB_INVALID_REQUEST, "unsupported game / num_players combination (RB_FLAG_LANE_PER_SESSION: A/B builds only)");
   const bool fanout = (cfg->flags & RB_P2P_FLAG_FANOUT) != 0;
   if (fanout && (!ops->fanout_supported || cfg->sparse_saving))
     return pfail(nullptr, RB_INVALID_REQUEST,
@@ -472,6 +472,11 @@ rb_status rb_p2p_run_ticks_packets(rb_p2p* b, int32_t n_ticks, const void* local
   if (b->cfg.sparse_saving || b->fanout || b->ds.interval > 0 || b->peer.on)
     return pfail(b, RB_INVALID_REQUEST,
                  "rb_p2p_run_ticks_packets: sparse saving, the fan-out and network reports take rb_p2p_run_ticks");
+  // a packet's reference input (frame start - 1) may be as old as the newest received frame -
+  // 2 * max_prediction (recv_inputs' retain, protocol.rs:684-686); the 128-entry input queue ring
+  // holds the newest 128 frames, so that frame must be younger than last - 127
+  if (2 * b->W >= kQueueLen)
+    return pfail(b, RB_INVALID_REQUEST, "rb_p2p_run_ticks_packets: needs 2 * max_prediction < 128 (the input ring)");
   P2PParams p = base_params(b);
   p.local_in = static_cast<const uint8_t*>(local_inputs);
   p.local_stride = local_stride;

@@ -55,6 +55,12 @@ __global__ void __launch_bounds__(256) decode_packets_kernel(const DecParams p) 
     p.status[s] = kDecNothing;
     return;
   }
+  // a length past the row would read the next endpoint's packet (or past the tensor): the
+  // datagram is not what the row holds, so it is malformed
+  if (n > p.packet_stride) {
+    p.status[s] = kDecMalformed;
+    return;
+  }
   // protocol.rs:639-642: a packet must not skip frames we never received
   if (last != kNull && last + 1 < start) {
     p.status[s] = kDecGap;

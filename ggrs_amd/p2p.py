@@ -121,10 +121,16 @@ class P2PSession(_StreamOrdered):
         lengths, start_frames [T, P, S] int32 (length 0: no packet)
         decode_status, acks   None or [P, S] int32 outputs: the last tick's decode
                       result per endpoint, the newest frame received per endpoint"""
+        import torch
         T = int(local_inputs.shape[0])
         assert tuple(local_inputs.shape[1:]) == (self.num_players, self.num_sessions)
         assert tuple(packets.shape[:3]) == (T, self.num_players, self.num_sessions) and packets.dim() == 4
         assert tuple(lengths.shape) == tuple(start_frames.shape) == (T, self.num_players, self.num_sessions)
+        # the kernel reads packets as bytes and lengths / start frames as int32, and writes int32 outputs
+        assert packets.dtype == torch.uint8, "packets must be uint8 (the row stride is a byte count)"
+        assert lengths.dtype == start_frames.dtype == torch.int32, "lengths and start_frames must be int32"
+        for o in (decode_status, acks):
+            assert o is None or o.dtype == torch.int32, "decode_status / acks must be int32"
         lp, lk = _dev_ptr(local_inputs)
         pp, pk = _dev_ptr(packets)
         np_, nk = _dev_ptr(lengths)

@@ -141,7 +141,7 @@ rb_status rb_advance_frame(rb_batch* b);
  * tick t reads its inputs at inputs + t*tick_stride_bytes, laid out
  * [num_players][num_sessions] Input values (host or device memory).  The host
  * bookkeeping runs tick by tick as in rb_advance_frame; consecutive
- * steady-state ticks (current frame > check_distance, 1 <= check_distance <= 8)
+ * steady-state ticks (current frame > check_distance, 1 <= check_distance <= 16)
  * execute as ONE fused device launch.  A session whose resimulation
  * mismatches stops advancing (as with per-tick calls) while the others run
  * on; with RB_FLAG_CHECKED the call returns RB_MISMATCHED_CHECKSUM if any
@@ -314,10 +314,13 @@ rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs,
  *   acks          NULL, or int32 [num_players][S]: after the call, the newest
  *                 frame received per endpoint (RB_NULL_FRAME: none), the ack
  *                 the receiver returns to the sender
- * A malformed packet panics its session (the reference's decode().expect,
- * "decoding failed"); a packet that skips frames never received is dropped
- * (status -2).  Sparse saving, the fan-out, desync detection and peers'
- * connect-status reports: RB_INVALID_REQUEST. */
+ * A malformed packet (or a length above packet_stride) panics its session
+ * (the reference's decode().expect, "decoding failed", protocol.rs:656); so
+ * does a packet that skips frames never received (status -2: the reference's
+ * assert!, protocol.rs:639-642).  Sparse saving, the fan-out, desync
+ * detection, peers' connect-status reports and max_prediction >= 64 (a
+ * reference input up to 2*max_prediction frames back must still be in the
+ * 128-entry input ring): RB_INVALID_REQUEST. */
 rb_status rb_p2p_run_ticks_packets(rb_p2p* b, int32_t n_ticks, const void* local_inputs, int64_t local_stride_bytes,
                                    const uint8_t* packets, int64_t packet_stride, const int32_t* lengths,
                                    const int32_t* start_frames, int32_t* decode_status, int32_t* acks);
@@ -426,7 +429,9 @@ rb_status rb_p2p_profile_take(rb_p2p* b, double* total_ms, int32_t* launches);
  * remote_inputs[frame][num_players][num_sessions] (input_bytes each) and
  * remote_upto advances: exactly the delivery tensors rb_p2p_run_ticks reads.
  * status[s]: 0 new inputs, 1 nothing new, -1 malformed (the reference panics:
- * "decoding failed"), -2 frames missing before start_frame (reference assert).
+ * "decoding failed"; also a length above packet_stride), -2 frames missing
+ * before start_frame (the reference asserts).  The caller decides what a
+ * negative status does to the session (nothing is decoded for it).
  * A packet whose reference input is older than 2*max_prediction frames is
  * ignored (recv_inputs retention, protocol.rs:686-688). */
 rb_status rb_decode_input_packets(int32_t device, void* stream, int32_t handle, int32_t num_players,
