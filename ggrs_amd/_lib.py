@@ -117,6 +117,7 @@ SIGNATURES = [
     ("rb_debug_corrupt_cell", _I32, [_P, _I32, _I32, _I32, ctypes.c_uint32]),
     ("rb_debug_sincosf", _I32, [_I32, _P, _P, _P, ctypes.c_int64]),
     ("rb_debug_speed_clamp", _I32, [_I32, _P, _P, _P, _P, ctypes.c_int64]),
+    ("rb_debug_exgame_inrange", _I32, [_I32, ctypes.c_uint32, ctypes.c_int64, _P]),
     ("rb_profile_enable", _I32, [_P, _I32]),
     ("rb_profile_take", _I32, [_P, ctypes.POINTER(ctypes.c_double), _PI32]),
     ("rb_register_game_plugin", _I32, [ctypes.c_char_p, _PI32]),

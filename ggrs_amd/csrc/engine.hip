@@ -67,6 +67,24 @@ __global__ void sincos_kernel(const float* __restrict__ x, float* __restrict__ s
   co[i] = r.c;
 }
 
+// The in-range forms the fused steady ticks and the fan-out run (ExGame::prepare / advance<true>):
+// for the floats with bits first + i, out[0][i] / out[1][i] = sincosf_glibc<true> (sin, cos),
+// out[2..3][i] = rem_euclid_near<true>(x +- ROTATION_SPEED, 2 pi), out[4..5][i] =
+// rem_euclid<true>(x +- ROTATION_SPEED, 2 pi) (rb_debug_exgame_inrange).
+__global__ void inrange_kernel(uint32_t first, int64_t n, float* __restrict__ out) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  using E = ExGame<2, true>;
+  const float x = __uint_as_float(first + static_cast<uint32_t>(i));
+  const SinCos r = sincosf_glibc<true>(x, nullptr);
+  out[i] = r.s;
+  out[n + i] = r.c;
+  out[2 * n + i] = rem_euclid_near<true>(x + E::kRotationSpeed, 2.0f * E::kPi);
+  out[3 * n + i] = rem_euclid_near<true>(x + -E::kRotationSpeed, 2.0f * E::kPi);
+  out[4 * n + i] = rem_euclid<true>(x + E::kRotationSpeed, 2.0f * E::kPi);
+  out[5 * n + i] = rem_euclid<true>(x - E::kRotationSpeed, 2.0f * E::kPi);
+}
+
 __global__ void clamp_kernel(const float* __restrict__ vx, const float* __restrict__ vy, float* __restrict__ ox,
                              float* __restrict__ oy, int64_t n) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -861,6 +879,18 @@ rb_status rb_debug_sincosf(int32_t device, const float* x, float* so, float* co,
                     [n](dim3 grid, float* da, float*, float* d1, float* d2, uint32_t* du) {
                       hipLaunchKernelGGL(sincos_kernel, grid, dim3(256), 0, nullptr, da, d1, d2, n, du);
                     });
+}
+
+rb_status rb_debug_exgame_inrange(int32_t device, uint32_t first_bits, int64_t n, float* dev_out) {
+  if (n <= 0 || !dev_out) return RB_INVALID_REQUEST;
+  // the in-range forms are exact on [+0, 6.5) only (games.hpp ExGame::in_range)
+  if (first_bits >= 0x40D00000u || static_cast<uint64_t>(first_bits) + static_cast<uint64_t>(n) > 0x40D00000ull)
+    return RB_INVALID_REQUEST;
+  if (hipSetDevice(device) != hipSuccess) return RB_DEVICE_ERROR;
+  hipLaunchKernelGGL(inrange_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, nullptr, first_bits, n,
+                     dev_out);
+  if (hipGetLastError() != hipSuccess) return RB_DEVICE_ERROR;
+  return hipDeviceSynchronize() == hipSuccess ? RB_OK : RB_DEVICE_ERROR;
 }
 
 rb_status rb_debug_speed_clamp(int32_t device, const float* vx, const float* vy, float* ox, float* oy, int64_t n) {

@@ -770,6 +770,13 @@ struct GameOpsT final : GameOps {
         return hipGetLastError();
       }
     }
+    if constexpr (!kSpec && !kSparse && !kNet && p2p_lds_queue<G>()) {
+      if (p.T == 1 && p.W <= kLiveMaxW && p.live_tick) {  // one tick per launch (live play): p2p_kernel kLive
+        hipLaunchKernelGGL((p2p_kernel<G, false, false, false, false, false, false, true>), dim3(grid), dim3(block), 0,
+                           st, p);
+        return hipGetLastError();
+      }
+    }
     hipLaunchKernelGGL((p2p_kernel<G, kSpec, kSparse, kNet, false, false>), dim3(grid), dim3(block), lds, st, p);
     return hipGetLastError();
   }
@@ -785,6 +792,11 @@ struct GameOpsT final : GameOps {
                                              static_cast<int>(lds));
           if (e != hipSuccess) return e;
           hipLaunchKernelGGL(k, dim3(grid), dim3(block), lds, st, p);
+          return hipGetLastError();
+        }
+        if (p.T == 1 && p.W <= kLiveMaxW && p.live_tick) {  // one tick per launch (live play): p2p_kernel kLive
+          hipLaunchKernelGGL((p2p_kernel<G, false, false, false, false, false, true, true>), dim3(grid), dim3(block), 0,
+                             st, p);
           return hipGetLastError();
         }
       }

@@ -328,6 +328,7 @@ struct P2PParams {
   uint32_t local_mask;
   int32_t sparse;
   int32_t sync_ticks;  // 1: lock-step ticks on the plain path too (no kAsync; A/B and tests)
+  int32_t live_tick;   // 1: one-tick launches take p2p_kernel kLive (RB_P2P_LIVE=0 at create: off, A/B and tests)
   DesyncParams ds;
   PeerParams peer;
   // kWire (rb_p2p_run_ticks_packets): the remote inputs arrive as the peers'
@@ -490,12 +491,12 @@ template <int IB>
 struct RingIO {
   uint8_t* ring;
   int P, Spad;
-  __device__ uint32_t get(int32_t f, int h, unsigned s) const {
+  __device__ __forceinline__ uint32_t get(int32_t f, int h, unsigned s) const {
     const size_t i = (static_cast<size_t>(f & (kQueueLen - 1)) * P + h) * Spad + s;
     if constexpr (IB == 4) return reinterpret_cast<const uint32_t*>(ring)[i];
     else return ring[i];
   }
-  __device__ void put(int32_t f, int h, unsigned s, uint32_t v) const {
+  __device__ __forceinline__ void put(int32_t f, int h, unsigned s, uint32_t v) const {
     const size_t i = (static_cast<size_t>(f & (kQueueLen - 1)) * P + h) * Spad + s;
     if constexpr (IB == 4) reinterpret_cast<uint32_t*>(ring)[i] = v;
     else ring[i] = static_cast<uint8_t>(v);
@@ -516,6 +517,51 @@ struct LdsRing {
     col[static_cast<unsigned>(f & (kQueueLen - 1)) * row] = static_cast<uint8_t>(v);
   }
 };
+// The input ring of a one-tick launch (p2p_kernel kLive): this lane's player's
+// 16 frames [lo, lo + 15] in registers (frame f is byte f & 15 of w), read from
+// the HBM ring in one round of loads before the tick issues any store.  Puts
+// inside the window stay there and are written back once, at the end of the
+// launch: on CDNA vmcnt retires loads and stores in issue order, so a load
+// issued after a store waits for the store too, and the tick's LoadGameState
+// would otherwise wait for the poll's ring stores.  Puts outside the window go
+// straight to HBM; reads outside it fall back to a load (only the dry
+// rollback of a PredictionThreshold tick predicts from a frame that old).
+struct WinRing {
+  RingIO<1> hbm;
+  mutable int32_t lo;
+  mutable uint32_t w0, w1, w2, w3;  // bytes 0-3, 4-7, 8-11, 12-15 (four scalars: no array for SROA to keep)
+  mutable uint32_t dirty;           // window bytes put in this launch
+  __device__ __forceinline__ uint32_t byte(uint32_t k) const {
+    // masks, not a select of the four words: a select between loads of one object's members folds
+    // into a load from a selected address, which keeps the object in memory (scratch, or LDS)
+    const uint32_t q = k >> 2;
+    const uint32_t x = (w0 & (q == 0u ? ~0u : 0u)) | (w1 & (q == 1u ? ~0u : 0u)) | (w2 & (q == 2u ? ~0u : 0u)) |
+                       (w3 & (q == 3u ? ~0u : 0u));
+    return (x >> (8u * (k & 3u))) & 0xFFu;
+  }
+  __device__ __forceinline__ int32_t frame_of(uint32_t k) const { return lo + ((static_cast<int32_t>(k) - lo) & 15); }
+  __device__ __forceinline__ uint32_t get(int32_t f, int h, unsigned s) const {
+    if (static_cast<uint32_t>(f - lo) < 16u) return byte(static_cast<uint32_t>(f) & 15u);
+    const uint32_t v = hbm.get(f, h, s);
+    settle(v);  // wait here, on this path only
+    return v;
+  }
+  __device__ __forceinline__ void put(int32_t f, int h, unsigned s, uint32_t v) const {
+    if (static_cast<uint32_t>(f - lo) < 16u) {
+      const uint32_t k = static_cast<uint32_t>(f) & 15u, q = k >> 2, sh = 8u * (k & 3u);
+      const uint32_t m = ~(0xFFu << sh), x = (v & 0xFFu) << sh;
+      w0 = q == 0u ? ((w0 & m) | x) : w0;
+      w1 = q == 1u ? ((w1 & m) | x) : w1;
+      w2 = q == 2u ? ((w2 & m) | x) : w2;
+      w3 = q == 3u ? ((w3 & m) | x) : w3;
+      dirty |= 1u << k;
+    } else {
+      hbm.put(f, h, s, v);
+    }
+  }
+};
+constexpr int kLiveMaxW = 15;  // the window holds frames cur - W .. cur (and the local add at cur + delay)
+
 // LDS queues: 1-byte inputs, one player per lane (ex_game lane per player, the brawler).
 template <class G>
 constexpr bool p2p_lds_queue() {
@@ -670,7 +716,9 @@ constexpr int kFanGroup = 4;  // branches a lane advances together (its independ
 // are compiled in only where the batch uses them (fewer live scalars: no SGPR
 // spills on the plain path)
 // Attribution builds (tools/mkvar.sh -DRB_P2P_EXP=...): 1 drops the game's
-// AdvanceFrame math, 2 its save checksum.  Always 0 in the product.
+// AdvanceFrame math, 2 its save checksum; one-tick launches (kLive): 8 skips the
+// input window and the tick (state loaded and stored back), 16 skips the tick,
+// 32 returns at entry (the launch floor).  Always 0 in the product.
 #ifndef RB_P2P_EXP
 #define RB_P2P_EXP 0
 #endif
@@ -692,11 +740,20 @@ constexpr int kFanGroup = 4;  // branches a lane advances together (its independ
 #ifndef RB_P2P_WAVES_PER_EU
 #define RB_P2P_WAVES_PER_EU 1  // >1: ask the compiler for that many waves per SIMD (VGPR cap; A/B builds)
 #endif
-template <class G, bool kSpec, bool kSparse, bool kNet, bool kLdsC, bool kAsync, bool kWire = false>
+// kLive: a launch of exactly one tick (live play: one advance_frame per
+// rendered frame, p2p_session.rs:253-371) with the cells in HBM, shaped for
+// the fewest dependent memory round trips: every load whose address is known
+// at entry (queue state, live state, deliveries, packets, work counters) is
+// issued first; then the input window (WinRing) and the delivered inputs;
+// then the rollback's LoadGameState; no store is issued before that load, and
+// no load after the first store.
+template <class G, bool kSpec, bool kSparse, bool kNet, bool kLdsC, bool kAsync, bool kWire = false, bool kLive = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RB_P2P_WAVES_PER_EU)))
 p2p_kernel(const P2PParams p) {
   static_assert(!kAsync || (kLdsC && !kSpec && !kNet), "lane-asynchronous ticks: plain or sparse path, LDS cells");
   static_assert(!kWire || (!kSpec && !kSparse && !kNet && !kAsync), "packet-fed ticks: the plain lock-step path");
+  static_assert(!kLive || (!kLdsC && !kAsync && !kSpec && !kSparse && !kNet && p2p_lds_queue<G>()),
+                "one-tick launches: the plain and packet-fed paths of lane-per-player games with 1-byte inputs");
   using InRec = typename G::InRec;
   using CS = typename G::CS;
   constexpr int NW = G::NWL;
@@ -713,6 +770,7 @@ p2p_kernel(const P2PParams p) {
   // process would have aborted): it reports RB_PANIC from then on and its
   // state, cells and queues stay as the panic left them.  (Checked once the
   // session's state loads are issued, so they do not wait for this one.)
+  if constexpr (kLive && (RB_P2P_EXP & 32)) return;  // (attribution builds only)
   const bool panicked = p.status[s] == kP2PStatusPanic;
   const unsigned Spad = static_cast<unsigned>(p.Spad), Gpad = Spad * L;
   const unsigned slot_words = static_cast<unsigned>(NW) * Gpad;
@@ -722,7 +780,8 @@ p2p_kernel(const P2PParams p) {
   const RingIO<IB> hbm{reinterpret_cast<uint8_t*>(p.ring), P, p.Spad};
   extern __shared__ uint8_t lds_queue[];
   const auto ring = [&]() __attribute__((always_inline)) {
-    if constexpr (kLdsQ) return LdsRing{lds_queue + threadIdx.x, blockDim.x};
+    if constexpr (kLive) return WinRing{hbm, 0, 0u, 0u, 0u, 0u, 0u};
+    else if constexpr (kLdsQ) return LdsRing{lds_queue + threadIdx.x, blockDim.x};
     else return hbm;
   }();
   // the in-kernel fan-out (the batch's branches are this kernel's own unless fan_generic)
@@ -783,6 +842,75 @@ p2p_kernel(const P2PParams p) {
     sm_player = p.spec_meta[SM_PLAYER * Spad + s];
 #pragma unroll
     for (int q = 0; q < 4; ++q) sm_cand[q] = static_cast<uint32_t>(p.spec_meta[(SM_CAND + q) * Spad + s]);
+  }
+  // ---- the per-tick delivery tensors, loaded one tick ahead: at the top of
+  // tick t, before its snapshot stores, come the delivered watermark and the
+  // local inputs of tick t+1; right after the poll, the first kPre remote
+  // frames tick t+1 will add (their frame numbers are known once the poll
+  // has moved the connection status).  Every lane loads (clamped, always
+  // valid addresses) and uses what its players need: a branch around a load
+  // would make the compiler wait for it at the join.
+  constexpr int kPre = 4;
+  const int first_local = p.local_mask ? __builtin_ctz(p.local_mask) : 0;
+  auto load_upto = [&](int t, int j) __attribute__((always_inline)) -> int32_t {
+    if constexpr (kWire) return kNullFrame;  // (no delivery tensors: packets)
+    const int h = min(player_of(j), P - 1);
+    return p.upto[static_cast<int64_t>(t) * p.upto_stride + static_cast<int64_t>(h) * p.S + s];
+  };
+  auto load_local = [&](int t, int j) __attribute__((always_inline)) -> uint32_t {
+    if (!p.local_mask) return 0u;  // launch-uniform
+    int h = player_of(j);
+    h = (h < P && ((p.local_mask >> h) & 1u)) ? h : first_local;
+    const uint8_t* src = p.local_in + static_cast<int64_t>(t) * p.local_stride + (static_cast<size_t>(h) * p.S + s) * IB;
+    return IB == 4 ? *reinterpret_cast<const uint32_t*>(src) : *src;
+  };
+  auto remote_start = [&](int j) __attribute__((always_inline)) {
+    return q[j].conn_last == kNullFrame ? p.remote_delay : q[j].conn_last + 1;
+  };
+  // remote_in[frame][P][S]: a per-lane base and a 32-bit frame stride (P * S * IB < 2^32),
+  // so an address is one 32x32->64 multiply-add
+  const uint32_t rstride = static_cast<uint32_t>(P) * static_cast<uint32_t>(p.S) * IB;
+  const uint8_t* rbase[PPL];
+#pragma unroll
+  for (int j = 0; j < PPL; ++j)
+    rbase[j] = kWire ? nullptr : p.remote_in + (static_cast<size_t>(min(player_of(j), P - 1)) * p.S + s) * IB;
+  auto load_remote = [&](int j, int32_t f) __attribute__((always_inline)) -> uint32_t {
+    if constexpr (kWire) return 0u;
+    f = max(0, min(f, p.remote_frames - 1));
+    const uint8_t* src = rbase[j] + static_cast<uint64_t>(static_cast<uint32_t>(f)) * rstride;
+    return IB == 4 ? *reinterpret_cast<const uint32_t*>(src) : *src;
+  };
+  // the first tick's watermark and local inputs (addresses known at entry: with the state loads)
+  int32_t up[PPL];
+  uint32_t lin[PPL], rv[PPL][kPre];
+#pragma unroll
+  for (int j = 0; j < PPL; ++j) {
+    up[j] = load_upto(0, j);
+    lin[j] = load_local(0, j);
+  }
+  // kWire + kLive: the first tick's packets with them (length, start frame, first 32 bytes)
+  struct PkHead {
+    int32_t n, start;
+    uint32_t w0[8];
+  };
+  auto wire_fetch = [&](int h, int t) __attribute__((always_inline)) -> PkHead {
+    PkHead r{0, 0, {}};
+    const size_t idx = (static_cast<size_t>(t) * P + static_cast<size_t>(h)) * static_cast<size_t>(p.S) + s;
+    r.n = p.pk_len[idx];
+    r.start = p.pk_start[idx];
+    const uint8_t* pk = p.packets + static_cast<int64_t>(idx) * p.packet_stride;
+    const uint4 a = reinterpret_cast<const uint4*>(pk)[0], b = reinterpret_cast<const uint4*>(pk)[1];
+    r.w0[0] = a.x, r.w0[1] = a.y, r.w0[2] = a.z, r.w0[3] = a.w, r.w0[4] = b.x, r.w0[5] = b.y, r.w0[6] = b.z, r.w0[7] = b.w;
+    return r;
+  };
+  [[maybe_unused]] PkHead pk_live{0, 0, {}};
+  if constexpr (kWire && kLive) pk_live = wire_fetch(min(player_of(0), P - 1), 0);
+  // kLive: the work counters this launch adds to, loaded with the rest (an update at the end
+  // would load them after every store of the tick)
+  [[maybe_unused]] unsigned long long st_pre[4] = {0ull, 0ull, 0ull, 0ull};
+  if constexpr (kLive) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) st_pre[i] = p.stats[i * Spad + s];
   }
   if (panicked) return;
   // LDS queue: the HBM frames this launch can read.  Reads are of frames
@@ -1117,43 +1245,6 @@ p2p_kernel(const P2PParams p) {
     }
   };
 
-  // ---- the per-tick delivery tensors, loaded one tick ahead: at the top of
-  // tick t, before its snapshot stores, come the delivered watermark and the
-  // local inputs of tick t+1; right after the poll, the first kPre remote
-  // frames tick t+1 will add (their frame numbers are known once the poll
-  // has moved the connection status).  Every lane loads (clamped, always
-  // valid addresses) and uses what its players need: a branch around a load
-  // would make the compiler wait for it at the join.
-  constexpr int kPre = 4;
-  const int first_local = p.local_mask ? __builtin_ctz(p.local_mask) : 0;
-  auto load_upto = [&](int t, int j) __attribute__((always_inline)) -> int32_t {
-    if constexpr (kWire) return kNullFrame;  // (no delivery tensors: packets)
-    const int h = min(player_of(j), P - 1);
-    return p.upto[static_cast<int64_t>(t) * p.upto_stride + static_cast<int64_t>(h) * p.S + s];
-  };
-  auto load_local = [&](int t, int j) __attribute__((always_inline)) -> uint32_t {
-    if (!p.local_mask) return 0u;  // launch-uniform
-    int h = player_of(j);
-    h = (h < P && ((p.local_mask >> h) & 1u)) ? h : first_local;
-    const uint8_t* src = p.local_in + static_cast<int64_t>(t) * p.local_stride + (static_cast<size_t>(h) * p.S + s) * IB;
-    return IB == 4 ? *reinterpret_cast<const uint32_t*>(src) : *src;
-  };
-  auto remote_start = [&](int j) __attribute__((always_inline)) {
-    return q[j].conn_last == kNullFrame ? p.remote_delay : q[j].conn_last + 1;
-  };
-  // remote_in[frame][P][S]: a per-lane base and a 32-bit frame stride (P * S * IB < 2^32),
-  // so an address is one 32x32->64 multiply-add
-  const uint32_t rstride = static_cast<uint32_t>(P) * static_cast<uint32_t>(p.S) * IB;
-  const uint8_t* rbase[PPL];
-#pragma unroll
-  for (int j = 0; j < PPL; ++j)
-    rbase[j] = kWire ? nullptr : p.remote_in + (static_cast<size_t>(min(player_of(j), P - 1)) * p.S + s) * IB;
-  auto load_remote = [&](int j, int32_t f) __attribute__((always_inline)) -> uint32_t {
-    if constexpr (kWire) return 0u;
-    f = max(0, min(f, p.remote_frames - 1));
-    const uint8_t* src = rbase[j] + static_cast<uint64_t>(static_cast<uint32_t>(f)) * rstride;
-    return IB == 4 ? *reinterpret_cast<const uint32_t*>(src) : *src;
-  };
   // desync detection after set_last_confirmed_frame (p2p_session.rs:313-316):
   // the lead lane runs it, the group learns whether it panicked
   [[maybe_unused]] CellSnap send_cells{};
@@ -1167,15 +1258,40 @@ p2p_kernel(const P2PParams p) {
       return group_min<L>(ok ? 1 : 0) == 1;
     }
   };
-  int32_t up[PPL];
-  uint32_t lin[PPL], rv[PPL][kPre];
 #pragma unroll
   for (int j = 0; j < PPL; ++j) {
-    up[j] = load_upto(0, j);
-    lin[j] = load_local(0, j);
     const int32_t f = remote_start(j);
 #pragma unroll
     for (int k = 0; k < kPre; ++k) rv[j][k] = load_remote(j, f + k);
+  }
+  if constexpr (kLive && !(RB_P2P_EXP & 8)) {  // the input window (frames cur - W .. cur of this lane's player), issued after the deliveries
+    const int hw = min(player_of(0), P - 1);
+    ring.lo = cur - W;
+    uint32_t b[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) b[k] = hbm.get(max(ring.frame_of(static_cast<uint32_t>(k)), 0), hw, s);
+    ring.w0 = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
+    ring.w1 = b[4] | (b[5] << 8) | (b[6] << 16) | (b[7] << 24);
+    ring.w2 = b[8] | (b[9] << 8) | (b[10] << 16) | (b[11] << 24);
+    ring.w3 = b[12] | (b[13] << 8) | (b[14] << 16) | (b[15] << 24);
+    // Everything the tick reads before its LoadGameState is in flight now; consume it here, in
+    // the entry block.  Otherwise the compiler sinks each load into the conditional block of its
+    // first use (the remote player's poll, past the window's wait), which costs a round trip.
+#pragma unroll
+    for (int j = 0; j < PPL; ++j) {
+      settle(static_cast<uint32_t>(up[j]));
+      settle(lin[j]);
+#pragma unroll
+      for (int k = 0; k < kPre; ++k) settle(rv[j][k]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) settle(static_cast<uint64_t>(st_pre[i]));
+    if constexpr (kWire) {
+      settle(static_cast<uint32_t>(pk_live.n));
+      settle(static_cast<uint32_t>(pk_live.start));
+#pragma unroll
+      for (int i = 0; i < 8; ++i) settle(pk_live.w0[i]);
+    }
   }
 
   // ---- kWire: UdpProtocol::on_input (protocol.rs:616-689) for the endpoint
@@ -1193,13 +1309,12 @@ p2p_kernel(const P2PParams p) {
       return kWireNothing;
     } else {
       const size_t idx = (static_cast<size_t>(t) * P + static_cast<size_t>(h)) * static_cast<size_t>(p.S) + s;
-      const int32_t n = p.pk_len[idx], start = p.pk_start[idx];
+      const PkHead hd = kLive ? pk_live : wire_fetch(h, t);  // (kLive: loaded at entry)
+      const int32_t n = hd.n, start = hd.start;
       const uint8_t* pk = p.packets + static_cast<int64_t>(idx) * p.packet_stride;
       uint32_t w0[8];
-      {
-        const uint4 a = reinterpret_cast<const uint4*>(pk)[0], b = reinterpret_cast<const uint4*>(pk)[1];
-        w0[0] = a.x, w0[1] = a.y, w0[2] = a.z, w0[3] = a.w, w0[4] = b.x, w0[5] = b.y, w0[6] = b.z, w0[7] = b.w;
-      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) w0[i] = hd.w0[i];
       if (q[j].disc || n <= 0) return kWireNothing;  // a disconnected player's endpoint no longer runs
       if (n > p.packet_stride) return kWirePanic;    // the row does not hold that many bytes
       const int32_t last = q[j].conn_last;
@@ -1327,13 +1442,15 @@ p2p_kernel(const P2PParams p) {
   // returns); false when the session stops on a reference panic.
   int32_t up_n[PPL];
   uint32_t lin_n[PPL], rv_n[PPL][kPre];
+  [[maybe_unused]] int32_t pk_ds = kWireNothing;  // kWire: the last tick's decode status of this lane's endpoint
+  uint32_t n_thr = 0;                             // PredictionThreshold ticks of this session in the launch
   // The tick's opening, through the PredictionThreshold decision: 0 = the
   // session stopped on a panic, 1 = the tick is over (Err(PredictionThreshold)),
   // 2 = rollback_and_save, add_local_input and the new frame follow.
   // The next tick's deliveries are prefetched, except by the P2P launches of
   // the two-launch fan-out (fanout_kernel), which are always of one tick (the
   // fan-out runs between ticks): there they would only hold registers.
-  constexpr bool kPrefetch = !kSpec || kInFan;
+  constexpr bool kPrefetch = (!kSpec || kInFan) && !kLive;
   auto tick_begin = [&](int t) __attribute__((always_inline)) -> int {
     const int tn = t + 1 < p.T ? t + 1 : t;
     if constexpr (kPrefetch) {
@@ -1353,7 +1470,7 @@ p2p_kernel(const P2PParams p) {
       if constexpr (kWire) {
         if (h < P && !((p.local_mask >> h) & 1u)) {
           const int32_t ds = wire_poll(j, h, t);
-          if (p.pk_status) p.pk_status[static_cast<size_t>(h) * p.S + s] = ds;
+          pk_ds = ds;  // (stored once, at the end of the launch)
           // the reference panics: "decoding failed" (protocol.rs:656) or the gap assert (:639-642)
           if (ds == kWirePanic || ds == kWireGap) status = kP2PStatusPanic;
         }
@@ -1484,7 +1601,7 @@ p2p_kernel(const P2PParams p) {
       status = kP2PStatusThreshold;  // Err(PredictionThreshold): the game does not move this tick
       load_frame = kNullFrame;       // and the user never sees the dropped requests
       nadv = nsave = 0;
-      if (lead) atomicAdd(&p.counters[0], 1u);
+      ++n_thr;  // (added to the batch counter once, at the end of the launch)
       if (!run_desync()) {  // desync detection ran before add_local_input failed (:313-316, :334)
         status = kP2PStatusPanic;
         return 0;
@@ -1671,7 +1788,9 @@ p2p_kernel(const P2PParams p) {
     tick_rotate();
     return true;
   };
-  if constexpr (!kAsync) {
+  if constexpr (kLive) {
+    if constexpr (!(RB_P2P_EXP & 24)) tick(0);  // (exactly one tick: no loop bound to branch on before the first use)
+  } else if constexpr (!kAsync) {
     for (int t = 0; t < p.T; ++t)
       if (!tick(t)) break;
   } else {
@@ -1746,6 +1865,14 @@ p2p_kernel(const P2PParams p) {
     }
   }
 
+  // ---- kLive: the window's frames put in this launch back to the HBM ring
+  if constexpr (kLive) {
+    const int hw = min(player_of(0), P - 1);
+    for (uint32_t d = ring.dirty; d; d &= d - 1) {
+      const uint32_t k = static_cast<uint32_t>(__builtin_ctz(d));
+      hbm.put(ring.frame_of(k), hw, s, ring.byte(k));
+    }
+  }
   // ---- LDS queue: the frames added in this launch back to the HBM ring
   if constexpr (kLdsQ) {
     const int h = player_of(0);
@@ -1783,7 +1910,14 @@ p2p_kernel(const P2PParams p) {
     *qrow(QF_LEN, h) = q[j].len;
     if constexpr (kNet) *qrow(QF_DISC, h) = q[j].disc ? 1 : 0;  // update_player_disconnects may set it
   }
-  if constexpr (kWire) {  // the newest frame received per endpoint: what the receiver acks
+  if constexpr (kWire) {  // the last tick's decode status and the newest frame received per endpoint (the ack)
+    if (p.pk_status) {
+#pragma unroll
+      for (int j = 0; j < PPL; ++j) {
+        const int h = player_of(j);
+        if (h < P && !((p.local_mask >> h) & 1u)) p.pk_status[static_cast<size_t>(h) * p.S + s] = pk_ds;
+      }
+    }
     if (p.acks) {
 #pragma unroll
       for (int j = 0; j < PPL; ++j) {
@@ -1802,10 +1936,18 @@ p2p_kernel(const P2PParams p) {
     p.trace[TR_NADV * Spad + s] = nadv;
     p.trace[TR_NSAVE * Spad + s] = nsave;
     if (status == kP2PStatusPanic) atomicAdd(&p.counters[2], 1u);
-    p.stats[ST_ADV * Spad + s] += tot_adv;
-    p.stats[ST_SAVE * Spad + s] += tot_save;
-    p.stats[ST_LOAD * Spad + s] += tot_load;
-    p.stats[ST_SELECT * Spad + s] += tot_sel;
+    if (n_thr) atomicAdd(&p.counters[0], n_thr);
+    if constexpr (kLive) {
+      p.stats[ST_ADV * Spad + s] = st_pre[ST_ADV] + tot_adv;
+      p.stats[ST_SAVE * Spad + s] = st_pre[ST_SAVE] + tot_save;
+      p.stats[ST_LOAD * Spad + s] = st_pre[ST_LOAD] + tot_load;
+      p.stats[ST_SELECT * Spad + s] = st_pre[ST_SELECT] + tot_sel;
+    } else {
+      p.stats[ST_ADV * Spad + s] += tot_adv;
+      p.stats[ST_SAVE * Spad + s] += tot_save;
+      p.stats[ST_LOAD * Spad + s] += tot_load;
+      p.stats[ST_SELECT * Spad + s] += tot_sel;
+    }
     if constexpr (kInFan) {
       if (in_fan) {  // the branches' metadata for the next launch's first tick
         p.stats[ST_BRANCH * Spad + s] += tot_branch;

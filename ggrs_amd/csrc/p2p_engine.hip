@@ -29,6 +29,7 @@ struct rb_p2p {
   bool fanout = false;
   bool sync_ticks = false;   // RB_P2P_SYNC_TICKS=1 at create: lock-step ticks (p2p.hpp kAsync off)
   bool fan_generic = false;  // RB_FANOUT_GENERIC=1 at create: fanout_kernel for every game
+  bool live_tick = true;     // RB_P2P_LIVE=0 at create: one-tick launches without p2p_kernel kLive (A/B, tests)
   uint32_t* spec_state = nullptr;
   uint32_t* spec_cells = nullptr;
   void* spec_cs = nullptr;
@@ -237,6 +238,7 @@ rb_status rb_p2p_create(const rb_p2p_config* cfg, rb_p2p** out) {
   b->fanout = fanout;
   if (const char* e = std::getenv("RB_P2P_SYNC_TICKS")) b->sync_ticks = std::atoi(e) != 0;
   if (const char* e = std::getenv("RB_FANOUT_GENERIC")) b->fan_generic = std::atoi(e) != 0;
+  if (const char* e = std::getenv("RB_P2P_LIVE")) b->live_tick = std::atoi(e) != 0;
   rb_p2p* bp = b.get();
   auto hip_fail = [&](hipError_t e, const char* what) {
     g_p2p_err = std::string(what) + ": " + hipGetErrorString(e);
@@ -384,6 +386,7 @@ P2PParams base_params(const rb_p2p* b) {
   p.local_mask = b->cfg.local_mask;
   p.sparse = b->cfg.sparse_saving != 0;
   p.sync_ticks = b->sync_ticks ? 1 : 0;
+  p.live_tick = b->live_tick ? 1 : 0;
   p.fan_generic = b->fan_generic ? 1 : 0;
   p.fan_k = b->cfg.fanout_candidates;
   p.spec_on = b->fanout ? 1 : 0;

@@ -196,6 +196,13 @@ rb_status rb_debug_corrupt_cell(rb_batch* b, int32_t session, int32_t frame, int
  * libm in the parity tests. */
 rb_status rb_debug_sincosf(int32_t device, const float* x, float* sin_out, float* cos_out, int64_t n);
 
+/* The in-range forms of the same arithmetic the fused steady ticks and the fan-out run
+ * (sincosf_glibc<true>, and the rotation step rem_euclid(x +- ROTATION_SPEED, 2 pi),
+ * ex_game.rs:282-296, as rem_euclid_near<true> and rem_euclid<true>) for the n floats whose
+ * bits are first_bits, first_bits + 1, ... (all in [+0, 6.5)), into device memory dev_out
+ * [6][n] (sin, cos, step up, step down, step up, step down).  Synchronises. */
+rb_status rb_debug_exgame_inrange(int32_t device, uint32_t first_bits, int64_t n, float* dev_out);
+
 /* Device evaluation of ex_game's speed clamp (ex_game.rs:300-304: v * MAX_SPEED
  * / |v| when |v| > MAX_SPEED) for n host (vx, vy) pairs — pins the short exact
  * sqrt/division sequences of device_math.hpp against host IEEE arithmetic. */

@@ -53,6 +53,7 @@ def load(path: str = LIB_PATH):
             "orc_cosf": (ctypes.c_float, [ctypes.c_float]),
             "orc_sinf": (ctypes.c_float, [ctypes.c_float]),
             "orc_sincosf_array": (None, [P, P, P, ctypes.c_int64]),
+            "orc_check_exgame_inrange": (ctypes.c_int64, [ctypes.c_uint32, ctypes.c_int64, P, I32, P]),
             "orc_batch_corrupt_cell": (I32, [P, I32, I32, I32, ctypes.c_uint32]),
             "orc_synth_inputs": (None, [U64, ctypes.c_uint32, I32, I32, I32, I32, I32, P]),
             "orc_bench_exgame": (ctypes.c_double, [I32, I32, I32, I32, I32, I32, I32, I32, U64, PI32]),
@@ -313,6 +314,17 @@ def sincosf(x: np.ndarray):
     c = np.empty_like(x)
     load().orc_sincosf_array(_ptr(x), _ptr(s), _ptr(c), x.size)
     return s, c
+
+
+def check_exgame_inrange(first_bits: int, dev: np.ndarray, threads: int):
+    """(mismatches, bits of the first mismatching float or None) of the device's in-range ex_game
+    arithmetic dev [6, n] (rb_debug_exgame_inrange) for the floats with bits first_bits + i
+    against this host's glibc sinf / cosf / fmodf (Rust's f32::sin / cos / rem_euclid)."""
+    dev = np.ascontiguousarray(dev, np.float32)
+    assert dev.ndim == 2 and dev.shape[0] == 6
+    fb = np.zeros(1, np.uint32)
+    n = load().orc_check_exgame_inrange(first_bits, dev.shape[1], _ptr(dev), threads, _ptr(fb))
+    return int(n), (None if fb[0] == 0xFFFFFFFF else int(fb[0]))
 
 
 def synth_inputs(seed: int, mask: int, S: int, P: int, T: int, f0: int = 0, input_bytes: int = 1) -> np.ndarray:

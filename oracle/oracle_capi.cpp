@@ -696,6 +696,52 @@ void orc_sincosf_array(const float* in, float* s, float* c, int64_t n) {
     c[i] = std::cos(in[i]);
   }
 }
+// Checker of the device's in-range ex_game arithmetic (rb_debug_exgame_inrange; tests/test_gpu_parity.py):
+// for the floats with bits first .. first + n - 1, the device's sin and cos (glibc sinf / cosf,
+// ex_game.rs:282-283) and the rotation steps rem_euclid(x + ROTATION_SPEED, 2 pi), rem_euclid(x -
+// ROTATION_SPEED, 2 pi) (ex_game.rs:291-296) as the steady kernel (rem_euclid_near) and the fan-out
+// (rem_euclid) compute them, in `dev` [6][n], against this host's glibc, bit for bit.  Returns the
+// mismatch count; *first_bad = the bits of the first mismatching float (0xFFFFFFFF: none).
+int64_t orc_check_exgame_inrange(uint32_t first, int64_t n, const float* dev, int32_t threads, uint32_t* first_bad) {
+  if (threads < 1) threads = 1;
+  std::vector<int64_t> bad(static_cast<size_t>(threads), 0);
+  std::vector<uint32_t> fb(static_cast<size_t>(threads), 0xFFFFFFFFu);
+  auto bits = [](float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    return u;
+  };
+  auto work = [&](int t) {
+    const int64_t lo = n * t / threads, hi = n * (t + 1) / threads;
+    for (int64_t i = lo; i < hi; ++i) {
+      const uint32_t xb = first + static_cast<uint32_t>(i);
+      float x;
+      std::memcpy(&x, &xb, 4);
+      const float want[6] = {std::sin(x),
+                             std::cos(x),
+                             exgame::rem_euclid(x + exgame::ROTATION_SPEED, 2.0f * exgame::PI),
+                             exgame::rem_euclid(x - exgame::ROTATION_SPEED, 2.0f * exgame::PI),
+                             exgame::rem_euclid(x + exgame::ROTATION_SPEED, 2.0f * exgame::PI),
+                             exgame::rem_euclid(x - exgame::ROTATION_SPEED, 2.0f * exgame::PI)};
+      bool ok = true;
+      for (int k = 0; k < 6; ++k) ok &= bits(dev[static_cast<int64_t>(k) * n + i]) == bits(want[k]);
+      if (!ok) {
+        if (bad[static_cast<size_t>(t)]++ == 0) fb[static_cast<size_t>(t)] = xb;
+      }
+    }
+  };
+  std::vector<std::thread> pool;
+  for (int t = 1; t < threads; ++t) pool.emplace_back(work, t);
+  work(0);
+  for (auto& th : pool) th.join();
+  int64_t total = 0;
+  *first_bad = 0xFFFFFFFFu;
+  for (int t = 0; t < threads; ++t) {
+    total += bad[static_cast<size_t>(t)];
+    if (*first_bad == 0xFFFFFFFFu) *first_bad = fb[static_cast<size_t>(t)];
+  }
+  return total;
+}
 int32_t orc_batch_corrupt_cell(void* b, int32_t session, int32_t frame, int32_t word, uint32_t m) {
   return static_cast<BatchBase*>(b)->corrupt_cell(session, frame, word, m);
 }

@@ -6,6 +6,8 @@ The engine restates glibc's sinf/cosf exactly (ggrs_amd/csrc/device_math.hpp),
 so ex_game is asserted BIT-EXACT here too (state images and fletcher16
 checksums), which implies the 1e-5 relative tolerance (asserted as well).
 """
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -92,6 +94,32 @@ def test_device_sincosf_bit_exact_with_glibc(gpu_available):
     bad_c = np.nonzero(gc.view(np.uint32) != hc.view(np.uint32))[0]
     assert bad_s.size == 0, (x[bad_s[:5]], gs[bad_s[:5]], hs[bad_s[:5]])
     assert bad_c.size == 0, (x[bad_c[:5]], gc[bad_c[:5]], hc[bad_c[:5]])
+
+
+def test_device_inrange_sincos_and_rotation_step_every_float(gpu_available):
+    """The in-range forms the timed steady kernel and the fan-out run (sincosf_glibc<true>,
+    rem_euclid_near<true>, rem_euclid<true>; ex_game.rs:282-296) evaluated ON THE DEVICE for every
+    float in [+0, 6.5) (1,087,373,312 values: every rotation an in-range tick can meet), bit for bit
+    against this host's glibc sinf / cosf and f32::rem_euclid (fmodf)."""
+    import os
+
+    import torch
+    from ggrs_amd import _lib as L
+    lib = L.load()
+    end = 0x40D00000  # bits of 6.5f: [+0, 6.5) is bits [0, end)
+    chunk = 1 << 25
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    out = torch.empty(6 * chunk, dtype=torch.float32, device="cuda")  # [6][n] packed per chunk
+    host = torch.empty(6 * chunk, dtype=torch.float32, pin_memory=True)
+    total = 0
+    for first in range(0, end, chunk):
+        n = min(chunk, end - first)
+        assert lib.rb_debug_exgame_inrange(0, first, n, ctypes.c_void_p(out.data_ptr())) == 0
+        host[:6 * n].copy_(out[:6 * n])
+        bad, fb = O.check_exgame_inrange(first, host[:6 * n].numpy().reshape(6, n), threads)
+        assert bad == 0, (bad, hex(fb), np.uint32(fb).view(np.float32))
+        total += n
+    assert total == end
 
 
 def test_device_speed_clamp_bit_exact(gpu_available):

@@ -216,10 +216,10 @@ def test_gpu_p2p_fed_through_the_wire_equals_direct_delivery(gpu_available, P, m
     assert wired.totals()[2] > 0  # rollbacks happened on the wire-fed batch too
 
 
-def _encode_schedule(lib, P, S, T, mask, rd, upto, dr, stride, seed):
+def _encode_schedule(lib, P, S, T, mask, rd, upto, dr, stride, seed, max_redo=2):
     """Every tick's packets, encoded on the device ahead of the ticks: remote
     handle h sends frames acked+1 .. upto[t, h], acked = the frame it knows
-    the receiver had one tick earlier minus 0-2 re-sent frames (an un-acked
+    the receiver had one tick earlier minus 0-max_redo re-sent frames (an un-acked
     sender); [T, P, S, stride] packets and [T, P, S] lengths / start frames."""
     import ctypes
 
@@ -236,7 +236,7 @@ def _encode_schedule(lib, P, S, T, mask, rd, upto, dr, stride, seed):
             if (mask >> h) & 1:
                 continue
             prev = du[t - 1, h] if t > 0 else torch.full((S,), -1, dtype=torch.int32, device="cuda")
-            redo = torch.from_numpy(rng.integers(0, 3, S).astype(np.int32)).cuda()
+            redo = torch.from_numpy(rng.integers(0, max_redo + 1, S).astype(np.int32)).cuda()
             acked = torch.where(prev < 0, prev, torch.clamp(prev - redo, min=rd - 1))
             acked = torch.where(acked < rd, torch.full_like(acked, -1), acked).contiguous()
             newest = du[t, h].contiguous()
@@ -336,3 +336,151 @@ def test_gpu_malformed_packet_panics_only_its_session(gpu_available):
     np.testing.assert_array_equal(wired.read_live()[ok], direct.read_live()[ok])
     with pytest.raises(G.InvalidRequest):  # packets need 16-byte rows of at least 32 bytes
         wired.run_ticks_packets(di[:1], pk[:1, :, :, :16], ln[:1], st[:1])
+
+
+def _oracle_packet_deliveries(P, S, T, mask, W, F, pk, ln, st):
+    """UdpProtocol::on_input (protocol.rs:616-689) restated on the host for every tick's packet
+    of every remote endpoint (on_input_reference): per tick the receiver's newest frame per
+    endpoint and its inputs by frame, exactly what the oracle's P2PSession is then delivered;
+    plus the decode status per (tick, handle, session)."""
+    pk_h, ln_h, st_h = pk.cpu().numpy(), ln.cpu().numpy(), st.cpu().numpy()
+    recv = np.zeros((F, P, S), np.uint8)
+    last = np.full((P, S), -1, np.int32)
+    uptos = np.full((T, P, S), -1, np.int32)
+    codes = np.ones((T, P, S), np.int32)
+    recvs = []
+    for t in range(T):
+        for h in range(P):
+            if (mask >> h) & 1:
+                continue
+            for s_ in range(S):
+                n = int(ln_h[t, h, s_])
+                start = int(st_h[t, h, s_])
+                refin = bytes([recv[start - 1, h, s_]]) if start >= 1 else bytes(1)
+                out, nl, code = on_input_reference(int(last[h, s_]), start, pk_h[t, h, s_, :n].tobytes(), refin, W, 1)
+                codes[t, h, s_] = code
+                for f, b in out.items():
+                    recv[f, h, s_] = b[0]
+                last[h, s_] = nl
+        uptos[t] = last
+        recvs.append(recv.copy())
+    return uptos, recvs, codes
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P,mask,rd,W,stride,max_redo,chunks", [
+    (2, 0b01, 2, 8, 32, 2, (1,) * 40 + (20, 20)),        # one-tick launches (live play), then multi-tick
+    (4, 0b0001, 1, 8, 32, 2, (1,) * 30 + (26, 24)),
+    (2, 0b01, 1, 15, 64, 28, (1,) * 50 + (30,)),        # long re-send windows: packets past 32 bytes, multi-segment
+    (3, 0b010, 0, 16, 64, 30, (1,) * 20 + (60,)),        # W > 15: the general one-tick kernel
+])
+def test_gpu_packet_ticks_match_oracle_p2p(gpu_available, P, mask, rd, W, stride, max_redo, chunks):
+    """rb_p2p_run_ticks_packets against the oracle, not against another device path: every
+    packet is decoded on the host by UdpProtocol::on_input's restatement and delivered to the
+    oracle's P2PSession (p2p_session.rs:253-371), the device decodes the same packets inside its
+    ticks; statuses, rollback frames, request counts, decode statuses and acks must agree after
+    every call, and cells, states and input queues after every call too."""
+    import torch
+
+    import ggrs_amd as G
+    from ggrs_amd import _lib as L
+    from ggrs_amd.p2p import PlayerType, synth_network
+    from test_p2p import compare_state, drive_oracle  # noqa: F401  (the P2P parity helpers)
+    lib = L.load()
+    S = 192
+    T = sum(chunks)
+    inputs, upto, rin = synth_network(S, P, T, mask, rd, 1, 5)
+    F = rin.shape[0]
+    b = (G.SessionBuilder(G.Game.EX_GAME, num_sessions=S).with_num_players(P).with_max_prediction_window(W)
+         .with_input_delay(1).with_remote_input_delay(rd))
+    for hh in range(P):
+        b.add_player(PlayerType.Local if (mask >> hh) & 1 else PlayerType.Remote, hh)
+    wired = b.start_p2p_session()
+    orc = O.OracleP2P(O.EX_GAME, P, W, 1, mask, S, sparse_saving=False, remote_delay=rd)
+    di, dr = torch.from_numpy(inputs).cuda(), torch.from_numpy(rin).cuda()
+    pk, ln, st = _encode_schedule(lib, P, S, T, mask, rd, upto, dr, stride, seed=11 + P, max_redo=max_redo)
+    if max_redo > 20:
+        assert int(ln.max()) > 32, "the schedule must produce packets past the 32-byte register window"
+    uptos, recvs, codes = _oracle_packet_deliveries(P, S, T, mask, W, F, pk, ln, st)
+    assert (codes >= 0).all()
+    dstat = torch.zeros((P, S), dtype=torch.int32, device="cuda")
+    acks = torch.full((P, S), -1, dtype=torch.int32, device="cuda")
+    remotes = [hh for hh in range(P) if not (mask >> hh) & 1]
+    t = 0
+    for n in chunks:
+        wired.run_ticks_packets(di[t:t + n], pk[t:t + n], ln[t:t + n], st[t:t + n], dstat, acks)
+        for k in range(t, t + n):
+            for hh in remotes:
+                assert orc.deliver(hh, uptos[k, hh], recvs[k][:, hh, :]) == 0, orc.last_panic()
+            for hh in range(P):
+                if (mask >> hh) & 1:
+                    assert orc.add_local_input(hh, inputs[k, hh]) == 0
+            ost, olf, ona, ons = orc.advance()
+        t += n
+        st_, lf, na, ns = wired.status()
+        np.testing.assert_array_equal(st_, ost, err_msg=f"status, tick {t - 1}")
+        np.testing.assert_array_equal(lf, olf, err_msg=f"LoadGameState frame, tick {t - 1}")
+        np.testing.assert_array_equal(na, ona, err_msg=f"AdvanceFrame count, tick {t - 1}")
+        np.testing.assert_array_equal(ns, ons, err_msg=f"SaveGameState count, tick {t - 1}")
+        np.testing.assert_array_equal(dstat.cpu().numpy()[remotes], codes[t - 1][remotes], err_msg=f"decode, tick {t - 1}")
+        np.testing.assert_array_equal(acks.cpu().numpy()[remotes], uptos[t - 1][remotes], err_msg=f"acks, tick {t - 1}")
+        if n > 1 or t % 10 == 0 or t == T:
+            compare_state(wired, orc, t - 1)
+    assert wired.totals()[2] > 0 and wired.counters()[2] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ticks_per_call", [1, 30], ids=["live", "fused"])
+def test_gpu_bad_packets_panic_like_the_reference(gpu_available, ticks_per_call):
+    """Packets the reference would panic on panic exactly their own session: a packet whose
+    start frame skips frames never received (assert!, protocol.rs:639-642), a length past the
+    packet row (the row cannot hold the datagram), and a multi-segment packet longer than 32
+    bytes whose last literal runs past its end (decode().expect, :656) — the general decoder,
+    not the single-segment fast path.  Every other session equals a directly fed batch."""
+    import torch
+
+    import ggrs_amd as G
+    from ggrs_amd import _lib as L
+    from ggrs_amd.p2p import PlayerType, synth_network
+    lib = L.load()
+    S, P, W, T, stride, mask, rd = 256, 2, 8, 60, 64, 0b01, 1
+    inputs, upto, rin = synth_network(S, P, T, mask, rd, 1, 4)
+
+    def batch():
+        b = (G.SessionBuilder(G.Game.EX_GAME, num_sessions=S).with_num_players(P).with_max_prediction_window(W)
+             .with_input_delay(1).with_remote_input_delay(rd))
+        b.add_player(PlayerType.Local, 0)
+        b.add_player(PlayerType.Remote, 1)
+        return b.start_p2p_session()
+
+    direct, wired = batch(), batch()
+    di, du, dr = (torch.from_numpy(a).cuda() for a in (inputs, upto, rin))
+    pk, ln, st = _encode_schedule(lib, P, S, T, mask, rd, upto, dr, stride, seed=21)
+    bad_t = 30
+    gap_s, long_s, seg_s = 5, 77, 150
+    for s_ in (gap_s, long_s, seg_s):
+        assert int(ln[bad_t, 1, s_]) > 0
+    st[bad_t, 1, gap_s] = upto[bad_t - 1, 1, gap_s] + 2  # skips the frame after the last one received
+    ln[bad_t, 1, long_s] = stride + 1                     # longer than its row
+    # literal(10) + run + literal claiming 40 bytes with 20 present: 33 bytes, malformed
+    body = [10 << 1] + list(range(1, 11)) + [(4 << 2) | 1] + [40 << 1] + list(range(20))
+    assert len(body) == 33
+    pk[bad_t, 1, seg_s, :] = 0
+    pk[bad_t, 1, seg_s, :len(body)] = torch.tensor(body, dtype=torch.uint8)
+    ln[bad_t, 1, seg_s] = len(body)
+    assert O.wire_decode(bytes(1), bytes(body)) is None
+    dstat = torch.zeros((P, S), dtype=torch.int32, device="cuda")
+    direct.run_ticks(di, du, dr)
+    t = 0
+    while t < T:
+        n = min(ticks_per_call, T - t)
+        wired.run_ticks_packets(di[t:t + n], pk[t:t + n], ln[t:t + n], st[t:t + n], dstat)
+        t += n
+    # a session stops at its panic: its decode status stays the panicking tick's
+    d = dstat.cpu().numpy()[1]
+    assert d[gap_s] == -2 and d[long_s] == -1 and d[seg_s] == -1, (d[gap_s], d[long_s], d[seg_s])
+    status = wired.status()[0]
+    dead = np.zeros(S, bool)
+    dead[[gap_s, long_s, seg_s]] = True
+    assert (status[dead] == 101).all() and wired.counters()[2] == 3
+    np.testing.assert_array_equal(wired.read_live()[~dead], direct.read_live()[~dead])
