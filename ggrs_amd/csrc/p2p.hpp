@@ -52,7 +52,11 @@ enum : int {
   QF_DISC = 6,         // ConnectionStatus::disconnected (0 / 1)
   QF_TAIL = 7,         // InputQueue: frame of inputs[tail] (input_queue.rs:83-101)
   QF_LEN = 8,          // InputQueue::length
-  QF_COUNT = 9,
+  // the fan-out's candidate list (not GGRS state): the queue's 16 most recent distinct
+  // inputs, newest first, as two u64 (4 rows), and their count
+  QF_MTF0 = 9,
+  QF_MTF_N = 13,
+  QF_COUNT = 14,
 };
 constexpr int kQsFields = QS_PLAYER0 + QF_COUNT * 4;
 // trace rows (the last tick of the last launch): LoadGameState frame, AdvanceFrame count, SaveGameState count
@@ -88,57 +92,59 @@ struct InputAlphabet<G, std::void_t<decltype(G::kInputAlphabet)>> {
   static constexpr uint32_t value = G::kInputAlphabet;
 };
 
-// The K candidate inputs of the speculated player h (K <= kSpecBranches,
-// 1-byte inputs): with an alphabet of at most K values, the alphabet in value
-// order (branch k = input k); otherwise the most recently confirmed distinct
-// values, newest first (the reference's prediction, repeat-last
-// (input_queue.rs:126-140), is candidate 0), looking back at most 32 frames
-// from the last added one, then the smallest values not yet taken.  Packed 4
-// per word, unused slots 0xFF with `n` = K.
-template <class R>
-__device__ __forceinline__ void fan_candidates(const R& ring, int h, unsigned s, int32_t la, uint32_t alphabet, int K,
+// The K candidate inputs of the speculated player (K <= kSpecBranches, 1-byte
+// inputs): with an alphabet of at most K values, the alphabet in value order
+// (branch k = input k); otherwise the most recently confirmed distinct values,
+// newest first (the reference's prediction, repeat-last, input_queue.rs:126-140,
+// is candidate 0) — the player's queue keeps them as a move-to-front list of
+// its 16 most recent distinct inputs, updated as each input is added (mtf_push),
+// so picking the candidates reads no input history — then, while the queue has
+// seen fewer than K distinct values, the smallest values not yet taken.  Packed
+// 4 per word, unused slots 0xFF.
+__device__ __forceinline__ void fan_candidates(uint64_t mlo, uint64_t mhi, int32_t mn, uint32_t alphabet, int K,
                                                uint32_t (&packed)[4]) {
-  uint32_t cand[kSpecBranches];
   if (alphabet <= static_cast<uint32_t>(K)) {
 #pragma unroll
-    for (int i = 0; i < kSpecBranches; ++i) cand[i] = static_cast<uint32_t>(i) < alphabet ? static_cast<uint32_t>(i) : 0xFFu;
-  } else {
-    uint64_t present[4] = {0ull, 0ull, 0ull, 0ull};  // values taken (alphabet <= 256)
-    int n = 0;
+    for (int w = 0; w < 4; ++w) {
+      uint32_t x = 0;
 #pragma unroll
-    for (int i = 0; i < kSpecBranches; ++i) cand[i] = 0xFFu;
-    constexpr int kBack = 32;
-    uint32_t hist[kBack];
-#pragma unroll
-    for (int d = 0; d < kBack; ++d) hist[d] = ring.get(max(la - d, 0), h, s);  // independent loads first
-#pragma unroll
-    for (int d = 0; d < kBack; ++d) {
-      const uint32_t v = hist[d] & 0xFFu;
-      const uint64_t word = present[v >> 6 & 3];
-      const bool take = la - d >= 0 && n < K && !((word >> (v & 63)) & 1ull);
-#pragma unroll
-      for (int i = 0; i < kSpecBranches; ++i) cand[i] = (take && i == n) ? v : cand[i];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) present[q] |= (take && q == static_cast<int>(v >> 6)) ? (1ull << (v & 63)) : 0ull;
-      n += take ? 1 : 0;
+      for (int b = 0; b < 4; ++b) {
+        const uint32_t i = static_cast<uint32_t>(4 * w + b);
+        x |= (i < alphabet ? i : 0xFFu) << (8 * b);
+      }
+      packed[w] = x;
     }
-    // fill: the smallest values of the alphabet not taken
+    return;
+  }
+  const int take = min(mn, K);  // the first `take` list entries, the rest 0xFF
+  const uint64_t klo = take >= 8 ? ~0ull : ((1ull << (8 * take)) - 1ull);
+  const uint64_t khi = take <= 8 ? 0ull : (take >= 16 ? ~0ull : ((1ull << (8 * (take - 8))) - 1ull));
+  uint64_t lo = (mlo & klo) | ~klo, hi = (mhi & khi) | ~khi;
+  if (take < K) {  // fill with the smallest values not taken (a queue that has seen fewer than K distinct inputs)
+    uint64_t present[4] = {0ull, 0ull, 0ull, 0ull};
 #pragma unroll
     for (int i = 0; i < kSpecBranches; ++i) {
-      if (i >= K) break;
+      const uint32_t v = static_cast<uint32_t>((i < 8 ? mlo >> (8 * i) : mhi >> (8 * (i - 8))) & 0xFFull);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) present[q] |= (i < take && q == static_cast<int>(v >> 6)) ? (1ull << (v & 63)) : 0ull;
+    }
+#pragma unroll
+    for (int i = 0; i < kSpecBranches; ++i) {
       int q = 0;
       while (q < 3 && present[q] == ~0ull) ++q;
       const uint32_t x = static_cast<uint32_t>(q * 64 + __builtin_ctzll(~present[q]));
-      const bool fill = i >= n && x < alphabet;
-      cand[i] = fill ? x : cand[i];
+      const bool fill = i >= take && i < K && x < alphabet;
+      const uint64_t m = 0xFFull << (8 * (i & 7)), xv = static_cast<uint64_t>(x) << (8 * (i & 7));
+      if (i < 8) lo = fill ? ((lo & ~m) | xv) : lo;
+      else hi = fill ? ((hi & ~m) | xv) : hi;
 #pragma unroll
       for (int w = 0; w < 4; ++w) present[w] |= (fill && w == q) ? (1ull << (x & 63)) : 0ull;
     }
   }
-#pragma unroll
-  for (int w = 0; w < 4; ++w)
-    packed[w] = (cand[4 * w] & 0xFFu) | ((cand[4 * w + 1] & 0xFFu) << 8) | ((cand[4 * w + 2] & 0xFFu) << 16) |
-                ((cand[4 * w + 3] & 0xFFu) << 24);
+  packed[0] = static_cast<uint32_t>(lo);
+  packed[1] = static_cast<uint32_t>(lo >> 32);
+  packed[2] = static_cast<uint32_t>(hi);
+  packed[3] = static_cast<uint32_t>(hi >> 32);
 }
 // The inputs a fan-out lane's player feeds its branch frames base .. base+7
 // (confirmed ones from the ring, the repeat-last prediction past the last
@@ -480,7 +486,33 @@ struct DevQueue {
   bool disc;  // ConnectionStatus::disconnected: rb_p2p_disconnect_player, or peers' reports (kNet)
   bool bad;
   int32_t tail, len;
+  // the fan-out's move-to-front list of the most recent distinct inputs (fan_candidates), kept
+  // only by fan-out batches whose alphabet is larger than K (mtf); bytes 0-7 / 8-15 newest first
+  bool mtf;
+  uint64_t mlo, mhi;
+  int32_t mn;
 };
+// Input v (1 byte) to the front of the queue's list: removed where it was, or the
+// entry past the list's end (the oldest of a full list) dropped, the entries
+// before it moved back one place.
+__device__ __forceinline__ void mtf_push(DevQueue& q, uint32_t v) {
+  v &= 0xFFu;
+  const uint64_t rep = 0x0101010101010101ull * v;
+  const uint64_t xl = q.mlo ^ rep, xh = q.mhi ^ rep;
+  const uint64_t zl = (xl - 0x0101010101010101ull) & ~xl & 0x8080808080808080ull;  // lowest zero byte: exact
+  const uint64_t zh = (xh - 0x0101010101010101ull) & ~xh & 0x8080808080808080ull;
+  int i = zl ? static_cast<int>(__builtin_ctzll(zl) >> 3) : (zh ? 8 + static_cast<int>(__builtin_ctzll(zh) >> 3) : 16);
+  if (i >= q.mn) {  // not in the list
+    i = min(q.mn, kSpecBranches - 1);
+    q.mn = min(q.mn + 1, kSpecBranches);
+  }
+  const int nb = i + 1;  // bytes 0 .. i are rewritten: byte 0 = v, bytes 1 .. i = the old bytes 0 .. i-1
+  const uint64_t klo = nb >= 8 ? 0ull : (~0ull << (8 * nb));
+  const uint64_t khi = nb <= 8 ? ~0ull : (nb >= 16 ? 0ull : (~0ull << (8 * (nb - 8))));
+  const uint64_t slo = q.mlo << 8, shi = (q.mhi << 8) | (q.mlo >> 56);
+  q.mlo = (q.mlo & klo) | (slo & ~klo) | v;
+  q.mhi = (q.mhi & khi) | (shi & ~khi);
+}
 // input_queue.rs:181 assert!(self.length <= INPUT_QUEUE_LENGTH): a caller of
 // the batch trips it by delivering remote inputs more than 128 frames past the
 // frames the session has discarded.  length only grows in add_input_by_frame,
@@ -620,6 +652,7 @@ constexpr bool p2p_lds_cells(int W, int block) {
 template <class R>
 __device__ __forceinline__ void q_add_by_frame(DevQueue& q, const R& r, int h, unsigned s, int32_t f, uint32_t v) {
   r.put(f, h, s, v);
+  if (q.mtf) mtf_push(q, v);
   q.last_added = f;
   q.len += 1;
   // the prediction bookkeeping as selects (no branch: every call site is in the hot poll)
@@ -817,6 +850,13 @@ p2p_kernel(const P2PParams p) {
       q[j].tail = *qrow(QF_TAIL, h);
       q[j].len = *qrow(QF_LEN, h);
       q[j].bad = false;
+      // the fan-out's candidate list, for an alphabet larger than K (launch-uniform)
+      q[j].mtf = kSpec && InputAlphabet<G>::value > static_cast<uint32_t>(p.fan_k);
+      if constexpr (kSpec) {
+        q[j].mlo = static_cast<uint32_t>(*qrow(QF_MTF0, h)) | static_cast<uint64_t>(static_cast<uint32_t>(*qrow(QF_MTF0 + 1, h))) << 32;
+        q[j].mhi = static_cast<uint32_t>(*qrow(QF_MTF0 + 2, h)) | static_cast<uint64_t>(static_cast<uint32_t>(*qrow(QF_MTF0 + 3, h))) << 32;
+        q[j].mn = *qrow(QF_MTF_N, h);
+      }
     } else {  // padding lane of a 4-lane group (P = 3): no player
       q[j] = DevQueue{kNullFrame, kNullFrame, kNullFrame, kNullFrame, INT32_MAX, 0u, false, 0};
     }
@@ -923,7 +963,7 @@ p2p_kernel(const P2PParams p) {
   if constexpr (kLdsQ) {
     const int h = player_of(0);
     // (and a packet's reference input, frame start - 1 >= last received - 2 * max_prediction)
-    const int32_t back = kWire ? 2 * W + 1 : ((in_fan && InputAlphabet<G>::value > static_cast<uint32_t>(p.fan_k)) ? 32 : 0);
+    const int32_t back = kWire ? 2 * W + 1 : 0;
     if (h < P && la0 != kNullFrame) {
       const int32_t lo = max(max(0, la0 - (kQueueLen - 1)), min(cur - W, la0) - back);
       for (int32_t f0 = lo; f0 <= la0; f0 += 8) {  // 8 loads in flight per round trip
@@ -1655,14 +1695,14 @@ p2p_kernel(const P2PParams p) {
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) cand[qq] = AC.packed[qq];
         nb = AC.n;
-      } else {
+      } else {  // the speculated player's candidate list, from its lane
+        const int src = lane_base + max(rs, 0);
+        const uint64_t mlo = static_cast<uint32_t>(__shfl(static_cast<int>(q[0].mlo), src, 64)) |
+                             static_cast<uint64_t>(static_cast<uint32_t>(__shfl(static_cast<int>(q[0].mlo >> 32), src, 64))) << 32;
+        const uint64_t mhi = static_cast<uint32_t>(__shfl(static_cast<int>(q[0].mhi), src, 64)) |
+                             static_cast<uint64_t>(static_cast<uint32_t>(__shfl(static_cast<int>(q[0].mhi >> 32), src, 64))) << 32;
         uint32_t raw[4];
-        if constexpr (kLdsQ) {
-          const LdsRing rr{lds_queue + (tid - static_cast<unsigned>(lane) + static_cast<unsigned>(max(rs, 0))), bd};
-          fan_candidates(rr, max(rs, 0), s, la_rs, InputAlphabet<G>::value, p.fan_k, raw);
-        } else {
-          fan_candidates(hbm, max(rs, 0), s, la_rs, InputAlphabet<G>::value, p.fan_k, raw);
-        }
+        fan_candidates(mlo, mhi, __shfl(q[0].mn, src, 64), InputAlphabet<G>::value, p.fan_k, raw);
         nb = cand_classes<G>(raw, p.fan_k, cand);
       }
       sm_valid = valid ? (1 | (nb << 8)) : 0;  // (the branch count rides along)
@@ -1909,6 +1949,15 @@ p2p_kernel(const P2PParams p) {
     *qrow(QF_TAIL, h) = q[j].tail;
     *qrow(QF_LEN, h) = q[j].len;
     if constexpr (kNet) *qrow(QF_DISC, h) = q[j].disc ? 1 : 0;  // update_player_disconnects may set it
+    if constexpr (kSpec) {
+      if (q[j].mtf) {
+        *qrow(QF_MTF0, h) = static_cast<int32_t>(q[j].mlo);
+        *qrow(QF_MTF0 + 1, h) = static_cast<int32_t>(q[j].mlo >> 32);
+        *qrow(QF_MTF0 + 2, h) = static_cast<int32_t>(q[j].mhi);
+        *qrow(QF_MTF0 + 3, h) = static_cast<int32_t>(q[j].mhi >> 32);
+        *qrow(QF_MTF_N, h) = q[j].mn;
+      }
+    }
   }
   if constexpr (kWire) {  // the last tick's decode status and the newest frame received per endpoint (the ack)
     if (p.pk_status) {
@@ -2033,7 +2082,12 @@ __global__ void __launch_bounds__(256) fanout_kernel(const FanParams p) {
   const bool valid = p.status[s] != kP2PStatusPanic && !any_disc && rs >= 0 && base < cur && base + W > cur && base >= 0 &&
                      p.tag[static_cast<unsigned>(base % W) * Spad + s] == base;
   uint32_t cand[4];  // the speculated player's candidates (every lane of the session computes the same)
-  fan_candidates(ring, max(rs, 0), s, la_rs, InputAlphabet<G>::value, p.fan_k, cand);
+  {
+    const int hr = max(rs, 0);
+    const uint64_t mlo = static_cast<uint32_t>(qrow(QF_MTF0, hr)) | static_cast<uint64_t>(static_cast<uint32_t>(qrow(QF_MTF0 + 1, hr))) << 32;
+    const uint64_t mhi = static_cast<uint32_t>(qrow(QF_MTF0 + 2, hr)) | static_cast<uint64_t>(static_cast<uint32_t>(qrow(QF_MTF0 + 3, hr))) << 32;
+    fan_candidates(mlo, mhi, qrow(QF_MTF_N, hr), InputAlphabet<G>::value, p.fan_k, cand);
+  }
   if (k == 0 && lane == 0) {
     p.spec_meta[SM_BASE * Spad + s] = base;
     p.spec_meta[SM_END * Spad + s] = cur;

@@ -290,6 +290,7 @@ rb_status rb_p2p_create(const rb_p2p_config* cfg, rb_p2p** out) {
       qs[(QS_PLAYER0 + QF_DISC * 4 + h) * Sp + s] = 0;  // ConnectionStatus::default: connected
       qs[(QS_PLAYER0 + QF_TAIL * 4 + h) * Sp + s] = 0;  // every queue's first input is frame 0
       qs[(QS_PLAYER0 + QF_LEN * 4 + h) * Sp + s] = 0;
+      qs[(QS_PLAYER0 + QF_MTF_N * 4 + h) * Sp + s] = 0;  // the fan-out's candidate list starts empty
     }
   }
   b->disconnected.assign(static_cast<size_t>(b->P) * b->S, 0);
