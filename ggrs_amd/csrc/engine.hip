@@ -231,6 +231,7 @@ rb_status launch_program(rb_batch* b, const TickProgram& tp, bool ingest, bool d
   p.nonce_base = (b->tick & 0xffffffu) << 8;
   p.debug = b->cfg.reserved[0];
   const bool timed = b->prof && (b->prof_tick++ % b->prof_every) == 0;  // sampled: an event pair costs host time
+  LaunchEv ev;  // the kernel's own start / end (hipExtLaunchKernel), no marker packets around it
   if (timed) {
     if (b->prof_used == b->prof_ev.size()) {
       hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -238,11 +239,10 @@ rb_status launch_program(rb_batch* b, const TickProgram& tp, bool ingest, bool d
       HIP_TRY(b, hipEventCreate(&e1));
       b->prof_ev.push_back({e0, e1});
     }
-    HIP_TRY(b, hipEventRecord(b->prof_ev[b->prof_used].first, b->stream));
+    ev = LaunchEv{b->prof_ev[b->prof_used].first, b->prof_ev[b->prof_used].second};
   }
-  HIP_TRY(b, b->ops->launch_tick(p, b->block, b->stream));
+  HIP_TRY(b, b->ops->launch_tick(p, b->block, b->stream, ev));
   if (timed) {
-    HIP_TRY(b, hipEventRecord(b->prof_ev[b->prof_used].second, b->stream));
     b->prof_ticks.resize(b->prof_ev.size());
     b->prof_ticks[b->prof_used] = 1;
     b->prof_used += 1;
@@ -556,6 +556,7 @@ rb_status launch_steady_run(rb_batch* b, const uint8_t* tick_inputs, int64_t str
   r.debug = b->cfg.reserved[0];
   r.pipe = b->pipe ? 1 : 0;
   const bool timed = b->prof;
+  LaunchEv ev;  // the kernel's own start / end (hipExtLaunchKernel), no marker packets around it
   if (timed) {
     if (b->prof_used == b->prof_ev.size()) {
       hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -563,12 +564,11 @@ rb_status launch_steady_run(rb_batch* b, const uint8_t* tick_inputs, int64_t str
       HIP_TRY(b, hipEventCreate(&e1));
       b->prof_ev.push_back({e0, e1});
     }
-    HIP_TRY(b, hipEventRecord(b->prof_ev[b->prof_used].first, b->stream));
+    ev = LaunchEv{b->prof_ev[b->prof_used].first, b->prof_ev[b->prof_used].second};
   }
-  hipError_t e = b->ops->launch_steady(r, b->cfg.check_distance, b->block, b->stream);
+  hipError_t e = b->ops->launch_steady(r, b->cfg.check_distance, b->block, b->stream, ev);
   if (e != hipSuccess) return fail(b, RB_DEVICE_ERROR, std::string("steady_kernel: ") + hipGetErrorString(e));
   if (timed) {
-    HIP_TRY(b, hipEventRecord(b->prof_ev[b->prof_used].second, b->stream));
     b->prof_ticks.resize(b->prof_ev.size());
     b->prof_ticks[b->prof_used] = n;
     b->prof_used += 1;

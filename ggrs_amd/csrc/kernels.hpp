@@ -20,6 +20,7 @@
 //   err   [Spad] i32          MismatchedChecksum{frame}, NULL_FRAME when healthy
 //   frozen[Spad/64] u64       sessions whose advance_frame returns Err (they no longer advance)
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <memory>
@@ -648,6 +649,21 @@ __global__ void report_kernel(const typename G::CS* __restrict__ cs, const int32
 #include "p2p.hpp"  // P2PSession kernel (uses load_words / store_words above)
 namespace rb {
 
+// Kernel timing (rb_profile_enable / rb_p2p_profile_enable): the events a launch
+// records itself through hipExtLaunchKernel — the kernel's own start and end,
+// with no marker packets of their own around it on the stream; both null when
+// the batch is not profiling.
+struct LaunchEv {
+  hipEvent_t start = nullptr, stop = nullptr;
+};
+template <class K, class... A>
+inline hipError_t rb_launch(K kernel, dim3 grid, dim3 block, uint32_t lds, hipStream_t st, const LaunchEv& ev,
+                            A... args) {
+  if (ev.start || ev.stop) hipExtLaunchKernelGGL(kernel, grid, block, lds, st, ev.start, ev.stop, 0u, args...);
+  else hipLaunchKernelGGL(kernel, grid, block, lds, st, args...);
+  return hipGetLastError();
+}
+
 struct GameOps {
   virtual ~GameOps() = default;
   int nw = 0, lanes = 1, players = 0, input_bytes = 0, inrec_bytes = 0, cs_bytes = 0, image_bytes = 0, canon_words = 0;
@@ -656,16 +672,17 @@ struct GameOps {
   virtual void init_words(uint32_t* w) const = 0;
   virtual void image(const uint32_t* w, int32_t frame, uint8_t* out) const = 0;
   virtual U128 cs_at(const void* arr, size_t i) const = 0;
-  virtual hipError_t launch_tick(const KParams& p, int block, hipStream_t st) const = 0;
+  virtual hipError_t launch_tick(const KParams& p, int block, hipStream_t st, const LaunchEv& ev = {}) const = 0;
   // fused steady-state ticks; hipErrorNotSupported when CD has no instantiation
-  virtual hipError_t launch_steady(const RunParams& p, int cd, int block, hipStream_t st) const = 0;
+  virtual hipError_t launch_steady(const RunParams& p, int cd, int block, hipStream_t st,
+                                   const LaunchEv& ev = {}) const = 0;
   static constexpr int kMaxFusedCD = 16;  // steady_kernel instantiations: check distances 1..16
   bool launch_steady_supported(int cd) const { return cd >= 1 && cd <= kMaxFusedCD; }
   virtual hipError_t launch_report(const void* cs, const int32_t* err, int S, int32_t frame, void* out,
                                    hipStream_t st) const = 0;
   // P2PSession ticks and the speculative fan-out (p2p.hpp); fan-out needs one
   // lane per player (ex_game), hipErrorNotSupported otherwise
-  virtual hipError_t launch_p2p(const P2PParams& p, int block, hipStream_t st) const = 0;
+  virtual hipError_t launch_p2p(const P2PParams& p, int block, hipStream_t st, const LaunchEv& ev = {}) const = 0;
   virtual hipError_t launch_fanout(const FanParams& p, int block, hipStream_t st) const = 0;
   bool fanout_supported = false;
   bool inlane_fanout = false;  // p2p_kernel runs the fan-out itself (inlane_fan), unless fan_generic
@@ -692,21 +709,17 @@ struct GameOpsT final : GameOps {
   U128 cs_at(const void* arr, size_t i) const override {
     return to_u128(reinterpret_cast<const typename G::CS*>(arr)[i]);
   }
-  hipError_t launch_tick(const KParams& p, int block, hipStream_t st) const override {
+  hipError_t launch_tick(const KParams& p, int block, hipStream_t st, const LaunchEv& ev) const override {
     const int grid = (p.Spad * G::kLanes + block - 1) / block;
-    if (p.in_mode == 2)
-      hipLaunchKernelGGL((tick_kernel<G, true>), dim3(grid), dim3(block), 0, st, p);
-    else
-      hipLaunchKernelGGL((tick_kernel<G, false>), dim3(grid), dim3(block), 0, st, p);
-    return hipGetLastError();
+    if (p.in_mode == 2) return rb_launch(tick_kernel<G, true>, dim3(grid), dim3(block), 0, st, ev, p);
+    return rb_launch(tick_kernel<G, false>, dim3(grid), dim3(block), 0, st, ev, p);
   }
   template <int CD>
-  static hipError_t steady_cd(const RunParams& p, int block, hipStream_t st) {
+  static hipError_t steady_cd(const RunParams& p, int block, hipStream_t st, const LaunchEv& ev) {
     const int grid = (p.Spad * G::kLanes + block - 1) / block;
     if (p.debug) {
 #if RB_EXPERIMENTS
-      hipLaunchKernelGGL((steady_kernel<G, CD, true>), dim3(grid), dim3(block), 0, st, p);
-      return hipGetLastError();
+      return rb_launch(steady_kernel<G, CD, true>, dim3(grid), dim3(block), 0, st, ev, p);
 #else
       return hipErrorNotSupported;  // experiment knobs need a RB_EXPERIMENTS=1 build
 #endif
@@ -714,32 +727,30 @@ struct GameOpsT final : GameOps {
 #if RB_EXPERIMENTS
     if constexpr (G::kHasPrep && HasFast<G>::value && CD >= 3 && CD <= 7 && CD % 2 == 1) {  // (an A/B variant)
       if (p.pipe) {
-        hipLaunchKernelGGL((steady_pipe_kernel<G, CD>), dim3(grid), dim3(block), 0, st, p);
-        return hipGetLastError();
+        return rb_launch(steady_pipe_kernel<G, CD>, dim3(grid), dim3(block), 0, st, ev, p);
       }
     }
 #endif
-    hipLaunchKernelGGL((steady_kernel<G, CD, false>), dim3(grid), dim3(block), 0, st, p);
-    return hipGetLastError();
+    return rb_launch(steady_kernel<G, CD, false>, dim3(grid), dim3(block), 0, st, ev, p);
   }
-  hipError_t launch_steady(const RunParams& p, int cd, int block, hipStream_t st) const override {
+  hipError_t launch_steady(const RunParams& p, int cd, int block, hipStream_t st, const LaunchEv& ev) const override {
     switch (cd) {
-      case 1: return steady_cd<1>(p, block, st);
-      case 2: return steady_cd<2>(p, block, st);
-      case 3: return steady_cd<3>(p, block, st);
-      case 4: return steady_cd<4>(p, block, st);
-      case 5: return steady_cd<5>(p, block, st);
-      case 6: return steady_cd<6>(p, block, st);
-      case 7: return steady_cd<7>(p, block, st);
-      case 8: return steady_cd<8>(p, block, st);
-      case 9: return steady_cd<9>(p, block, st);
-      case 10: return steady_cd<10>(p, block, st);
-      case 11: return steady_cd<11>(p, block, st);
-      case 12: return steady_cd<12>(p, block, st);
-      case 13: return steady_cd<13>(p, block, st);
-      case 14: return steady_cd<14>(p, block, st);
-      case 15: return steady_cd<15>(p, block, st);
-      case 16: return steady_cd<16>(p, block, st);
+      case 1: return steady_cd<1>(p, block, st, ev);
+      case 2: return steady_cd<2>(p, block, st, ev);
+      case 3: return steady_cd<3>(p, block, st, ev);
+      case 4: return steady_cd<4>(p, block, st, ev);
+      case 5: return steady_cd<5>(p, block, st, ev);
+      case 6: return steady_cd<6>(p, block, st, ev);
+      case 7: return steady_cd<7>(p, block, st, ev);
+      case 8: return steady_cd<8>(p, block, st, ev);
+      case 9: return steady_cd<9>(p, block, st, ev);
+      case 10: return steady_cd<10>(p, block, st, ev);
+      case 11: return steady_cd<11>(p, block, st, ev);
+      case 12: return steady_cd<12>(p, block, st, ev);
+      case 13: return steady_cd<13>(p, block, st, ev);
+      case 14: return steady_cd<14>(p, block, st, ev);
+      case 15: return steady_cd<15>(p, block, st, ev);
+      case 16: return steady_cd<16>(p, block, st, ev);
       default: return hipErrorNotSupported;
     }
   }
@@ -750,8 +761,8 @@ struct GameOpsT final : GameOps {
                        reinterpret_cast<rb_checksum_report*>(out));
     return hipGetLastError();
   }
-  template <bool kSpec, bool kSparse, bool kNet>
-  static hipError_t launch_p2p_as(const P2PParams& p, int grid, int block, hipStream_t st) {
+  template <bool kSpec, bool kSparse, bool kNet, bool kMtf = false>
+  static hipError_t launch_p2p_as_m(const P2PParams& p, int grid, int block, hipStream_t st, const LaunchEv& ev) {
     size_t lds = p2p_lds_bytes<G>(block);  // (the HBM-cell launches below)
     if constexpr ((!kSpec || inlane_fan<G>()) && !kNet && p2p_lds_queue<G>()) {
       // the snapshot ring in LDS (p2p_lds_cell_bytes) for launches of many ticks: it is copied in and
@@ -760,27 +771,31 @@ struct GameOpsT final : GameOps {
       if (p2p_lds_cells<G>(p.W, block) && p.T >= kLdsCellsMinTicks && (!kSpec || !p.fan_generic)) {
         // lane-asynchronous ticks (plain path and sparse saving) unless the batch asked for lock-step
         // ticks; the fan-out runs lock-step ticks
-        auto k = (!p.sync_ticks && !kSpec) ? p2p_kernel<G, kSpec, kSparse, kNet, true, !kSpec>
-                                           : p2p_kernel<G, kSpec, kSparse, kNet, true, false>;
+        auto k = (!p.sync_ticks && !kSpec) ? p2p_kernel<G, kSpec, kSparse, kNet, true, !kSpec, false, kMtf>
+                                           : p2p_kernel<G, kSpec, kSparse, kNet, true, false, false, kMtf>;
         lds = p2p_lds_bytes<G, true>(block) + p2p_lds_cell_bytes<G>(block, p.W);
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                            static_cast<int>(lds));
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k, dim3(grid), dim3(block), lds, st, p);
-        return hipGetLastError();
+        return rb_launch(k, dim3(grid), dim3(block), static_cast<uint32_t>(lds), st, ev, p);
       }
     }
-    if constexpr (!kSpec && !kSparse && !kNet && p2p_lds_queue<G>()) {
-      if (p.T == 1 && p.W <= kLiveMaxW && p.live_tick) {  // one tick per launch (live play): p2p_kernel kLive
-        hipLaunchKernelGGL((p2p_kernel<G, false, false, false, false, false, false, true>), dim3(grid), dim3(block), 0,
-                           st, p);
-        return hipGetLastError();
-      }
-    }
-    hipLaunchKernelGGL((p2p_kernel<G, kSpec, kSparse, kNet, false, false>), dim3(grid), dim3(block), lds, st, p);
-    return hipGetLastError();
+    return rb_launch(p2p_kernel<G, kSpec, kSparse, kNet, false, false, false, kMtf>, dim3(grid), dim3(block),
+                     static_cast<uint32_t>(lds), st, ev, p);
   }
-  hipError_t launch_p2p(const P2PParams& p, int block, hipStream_t st) const override {
+  // the fan-out's candidates: the alphabet itself when it has at most K values, else the queues'
+  // move-to-front lists (kMtf); ex_game (16 inputs) builds both, larger alphabets only the lists
+  template <bool kSpec, bool kSparse, bool kNet>
+  static hipError_t launch_p2p_as(const P2PParams& p, int grid, int block, hipStream_t st, const LaunchEv& ev) {
+    if constexpr (kSpec) {
+      if constexpr (InputAlphabet<G>::value > static_cast<uint32_t>(kSpecBranches))
+        return launch_p2p_as_m<kSpec, kSparse, kNet, true>(p, grid, block, st, ev);
+      else if (InputAlphabet<G>::value > static_cast<uint32_t>(p.fan_k))
+        return launch_p2p_as_m<kSpec, kSparse, kNet, true>(p, grid, block, st, ev);
+    }
+    return launch_p2p_as_m<kSpec, kSparse, kNet, false>(p, grid, block, st, ev);
+  }
+  hipError_t launch_p2p(const P2PParams& p, int block, hipStream_t st, const LaunchEv& ev) const override {
     const int grid = (p.Spad * G::kLanes + block - 1) / block;
     if (p.packets) {  // packet-fed ticks (rb_p2p_run_ticks_packets: the plain path, lock-step ticks)
       size_t lds = p2p_lds_bytes<G>(block);
@@ -791,28 +806,22 @@ struct GameOpsT final : GameOps {
           hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                              static_cast<int>(lds));
           if (e != hipSuccess) return e;
-          hipLaunchKernelGGL(k, dim3(grid), dim3(block), lds, st, p);
-          return hipGetLastError();
-        }
-        if (p.T == 1 && p.W <= kLiveMaxW && p.live_tick) {  // one tick per launch (live play): p2p_kernel kLive
-          hipLaunchKernelGGL((p2p_kernel<G, false, false, false, false, false, true, true>), dim3(grid), dim3(block), 0,
-                             st, p);
-          return hipGetLastError();
+          return rb_launch(k, dim3(grid), dim3(block), static_cast<uint32_t>(lds), st, ev, p);
         }
       }
-      hipLaunchKernelGGL((p2p_kernel<G, false, false, false, false, false, true>), dim3(grid), dim3(block), lds, st, p);
-      return hipGetLastError();
+      return rb_launch(p2p_kernel<G, false, false, false, false, false, true>, dim3(grid), dim3(block),
+                       static_cast<uint32_t>(lds), st, ev, p);
     }
     if (p.ds.interval > 0 || p.peer.on) {  // desync detection / peers' connect-status reports on
       if (p.sparse)  // sparse saving and the fan-out exclude each other (rb_p2p_create)
-        return launch_p2p_as<false, true, true>(p, grid, block, st);
+        return launch_p2p_as<false, true, true>(p, grid, block, st, ev);
       if (kFanout && p.spec_on && !p.peer.on)  // the fan-out assumes connected queues
-        return launch_p2p_as<kFanout, false, true>(p, grid, block, st);
-      return launch_p2p_as<false, false, true>(p, grid, block, st);
+        return launch_p2p_as<kFanout, false, true>(p, grid, block, st, ev);
+      return launch_p2p_as<false, false, true>(p, grid, block, st, ev);
     }
-    if (p.sparse) return launch_p2p_as<false, true, false>(p, grid, block, st);
-    if (kFanout && p.spec_on) return launch_p2p_as<kFanout, false, false>(p, grid, block, st);
-    return launch_p2p_as<false, false, false>(p, grid, block, st);
+    if (p.sparse) return launch_p2p_as<false, true, false>(p, grid, block, st, ev);
+    if (kFanout && p.spec_on) return launch_p2p_as<kFanout, false, false>(p, grid, block, st, ev);
+    return launch_p2p_as<false, false, false>(p, grid, block, st, ev);
   }
   // fan-out: one lane per player (ex_game) or one wave per session (the brawler), 1-byte inputs
   static constexpr bool kFanout = ((G::kLanes > 1 && G::kLanes <= 4) || G::kLanes == 64) && G::kInputBytes == 1;

@@ -101,6 +101,30 @@ struct InputAlphabet<G, std::void_t<decltype(G::kInputAlphabet)>> {
 // so picking the candidates reads no input history — then, while the queue has
 // seen fewer than K distinct values, the smallest values not yet taken.  Packed
 // 4 per word, unused slots 0xFF.
+// The fill of fan_candidates: the smallest values of the alphabet not among the first `take` list
+// entries, into list slots take .. K-1.  Out of line: it runs only while a queue has seen fewer
+// than K distinct inputs, and its bitmaps would otherwise hold registers in the fan-out kernels.
+struct CandList {
+  uint64_t lo, hi;
+};
+__device__ __noinline__ CandList fan_fill(uint64_t lo, uint64_t hi, int take, uint32_t alphabet, int K) {
+  uint64_t present[4] = {0ull, 0ull, 0ull, 0ull};
+  for (int i = 0; i < take; ++i) {
+    const uint32_t v = static_cast<uint32_t>((i < 8 ? lo >> (8 * i) : hi >> (8 * (i - 8))) & 0xFFull);
+    present[v >> 6] |= 1ull << (v & 63);
+  }
+  for (int i = take; i < K; ++i) {
+    int q = 0;
+    while (q < 3 && present[q] == ~0ull) ++q;
+    const uint32_t x = static_cast<uint32_t>(q * 64 + __builtin_ctzll(~present[q]));
+    if (x >= alphabet) break;
+    const uint64_t m = 0xFFull << (8 * (i & 7)), xv = static_cast<uint64_t>(x) << (8 * (i & 7));
+    if (i < 8) lo = (lo & ~m) | xv;
+    else hi = (hi & ~m) | xv;
+    present[q] |= 1ull << (x & 63);
+  }
+  return CandList{lo, hi};
+}
 __device__ __forceinline__ void fan_candidates(uint64_t mlo, uint64_t mhi, int32_t mn, uint32_t alphabet, int K,
                                                uint32_t (&packed)[4]) {
   if (alphabet <= static_cast<uint32_t>(K)) {
@@ -120,26 +144,10 @@ __device__ __forceinline__ void fan_candidates(uint64_t mlo, uint64_t mhi, int32
   const uint64_t klo = take >= 8 ? ~0ull : ((1ull << (8 * take)) - 1ull);
   const uint64_t khi = take <= 8 ? 0ull : (take >= 16 ? ~0ull : ((1ull << (8 * (take - 8))) - 1ull));
   uint64_t lo = (mlo & klo) | ~klo, hi = (mhi & khi) | ~khi;
-  if (take < K) {  // fill with the smallest values not taken (a queue that has seen fewer than K distinct inputs)
-    uint64_t present[4] = {0ull, 0ull, 0ull, 0ull};
-#pragma unroll
-    for (int i = 0; i < kSpecBranches; ++i) {
-      const uint32_t v = static_cast<uint32_t>((i < 8 ? mlo >> (8 * i) : mhi >> (8 * (i - 8))) & 0xFFull);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) present[q] |= (i < take && q == static_cast<int>(v >> 6)) ? (1ull << (v & 63)) : 0ull;
-    }
-#pragma unroll
-    for (int i = 0; i < kSpecBranches; ++i) {
-      int q = 0;
-      while (q < 3 && present[q] == ~0ull) ++q;
-      const uint32_t x = static_cast<uint32_t>(q * 64 + __builtin_ctzll(~present[q]));
-      const bool fill = i >= take && i < K && x < alphabet;
-      const uint64_t m = 0xFFull << (8 * (i & 7)), xv = static_cast<uint64_t>(x) << (8 * (i & 7));
-      if (i < 8) lo = fill ? ((lo & ~m) | xv) : lo;
-      else hi = fill ? ((hi & ~m) | xv) : hi;
-#pragma unroll
-      for (int w = 0; w < 4; ++w) present[w] |= (fill && w == q) ? (1ull << (x & 63)) : 0ull;
-    }
+  if (take < K) {  // a queue that has seen fewer than K distinct inputs
+    const CandList c = fan_fill(lo, hi, take, alphabet, K);
+    lo = c.lo;
+    hi = c.hi;
   }
   packed[0] = static_cast<uint32_t>(lo);
   packed[1] = static_cast<uint32_t>(lo >> 32);
@@ -334,7 +342,6 @@ struct P2PParams {
   uint32_t local_mask;
   int32_t sparse;
   int32_t sync_ticks;  // 1: lock-step ticks on the plain path too (no kAsync; A/B and tests)
-  int32_t live_tick;   // 1: one-tick launches take p2p_kernel kLive (RB_P2P_LIVE=0 at create: off, A/B and tests)
   DesyncParams ds;
   PeerParams peer;
   // kWire (rb_p2p_run_ticks_packets): the remote inputs arrive as the peers'
@@ -549,51 +556,6 @@ struct LdsRing {
     col[static_cast<unsigned>(f & (kQueueLen - 1)) * row] = static_cast<uint8_t>(v);
   }
 };
-// The input ring of a one-tick launch (p2p_kernel kLive): this lane's player's
-// 16 frames [lo, lo + 15] in registers (frame f is byte f & 15 of w), read from
-// the HBM ring in one round of loads before the tick issues any store.  Puts
-// inside the window stay there and are written back once, at the end of the
-// launch: on CDNA vmcnt retires loads and stores in issue order, so a load
-// issued after a store waits for the store too, and the tick's LoadGameState
-// would otherwise wait for the poll's ring stores.  Puts outside the window go
-// straight to HBM; reads outside it fall back to a load (only the dry
-// rollback of a PredictionThreshold tick predicts from a frame that old).
-struct WinRing {
-  RingIO<1> hbm;
-  mutable int32_t lo;
-  mutable uint32_t w0, w1, w2, w3;  // bytes 0-3, 4-7, 8-11, 12-15 (four scalars: no array for SROA to keep)
-  mutable uint32_t dirty;           // window bytes put in this launch
-  __device__ __forceinline__ uint32_t byte(uint32_t k) const {
-    // masks, not a select of the four words: a select between loads of one object's members folds
-    // into a load from a selected address, which keeps the object in memory (scratch, or LDS)
-    const uint32_t q = k >> 2;
-    const uint32_t x = (w0 & (q == 0u ? ~0u : 0u)) | (w1 & (q == 1u ? ~0u : 0u)) | (w2 & (q == 2u ? ~0u : 0u)) |
-                       (w3 & (q == 3u ? ~0u : 0u));
-    return (x >> (8u * (k & 3u))) & 0xFFu;
-  }
-  __device__ __forceinline__ int32_t frame_of(uint32_t k) const { return lo + ((static_cast<int32_t>(k) - lo) & 15); }
-  __device__ __forceinline__ uint32_t get(int32_t f, int h, unsigned s) const {
-    if (static_cast<uint32_t>(f - lo) < 16u) return byte(static_cast<uint32_t>(f) & 15u);
-    const uint32_t v = hbm.get(f, h, s);
-    settle(v);  // wait here, on this path only
-    return v;
-  }
-  __device__ __forceinline__ void put(int32_t f, int h, unsigned s, uint32_t v) const {
-    if (static_cast<uint32_t>(f - lo) < 16u) {
-      const uint32_t k = static_cast<uint32_t>(f) & 15u, q = k >> 2, sh = 8u * (k & 3u);
-      const uint32_t m = ~(0xFFu << sh), x = (v & 0xFFu) << sh;
-      w0 = q == 0u ? ((w0 & m) | x) : w0;
-      w1 = q == 1u ? ((w1 & m) | x) : w1;
-      w2 = q == 2u ? ((w2 & m) | x) : w2;
-      w3 = q == 3u ? ((w3 & m) | x) : w3;
-      dirty |= 1u << k;
-    } else {
-      hbm.put(f, h, s, v);
-    }
-  }
-};
-constexpr int kLiveMaxW = 15;  // the window holds frames cur - W .. cur (and the local add at cur + delay)
-
 // LDS queues: 1-byte inputs, one player per lane (ex_game lane per player, the brawler).
 template <class G>
 constexpr bool p2p_lds_queue() {
@@ -749,9 +711,8 @@ constexpr int kFanGroup = 4;  // branches a lane advances together (its independ
 // are compiled in only where the batch uses them (fewer live scalars: no SGPR
 // spills on the plain path)
 // Attribution builds (tools/mkvar.sh -DRB_P2P_EXP=...): 1 drops the game's
-// AdvanceFrame math, 2 its save checksum; one-tick launches (kLive): 8 skips the
-// input window and the tick (state loaded and stored back), 16 skips the tick,
-// 32 returns at entry (the launch floor).  Always 0 in the product.
+// AdvanceFrame math, 2 its save checksum, 32 returns at entry (the launch
+// floor).  Always 0 in the product.
 #ifndef RB_P2P_EXP
 #define RB_P2P_EXP 0
 #endif
@@ -773,20 +734,14 @@ constexpr int kFanGroup = 4;  // branches a lane advances together (its independ
 #ifndef RB_P2P_WAVES_PER_EU
 #define RB_P2P_WAVES_PER_EU 1  // >1: ask the compiler for that many waves per SIMD (VGPR cap; A/B builds)
 #endif
-// kLive: a launch of exactly one tick (live play: one advance_frame per
-// rendered frame, p2p_session.rs:253-371) with the cells in HBM, shaped for
-// the fewest dependent memory round trips: every load whose address is known
-// at entry (queue state, live state, deliveries, packets, work counters) is
-// issued first; then the input window (WinRing) and the delivered inputs;
-// then the rollback's LoadGameState; no store is issued before that load, and
-// no load after the first store.
-template <class G, bool kSpec, bool kSparse, bool kNet, bool kLdsC, bool kAsync, bool kWire = false, bool kLive = false>
+// kMtf (fan-out batches only): the candidates come from the queues' move-to-front lists, for an
+// alphabet larger than K; otherwise (ex_game at K = 16) they are the alphabet itself, and the lists
+// are neither kept nor read (no registers held for them).
+template <class G, bool kSpec, bool kSparse, bool kNet, bool kLdsC, bool kAsync, bool kWire = false, bool kMtf = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RB_P2P_WAVES_PER_EU)))
 p2p_kernel(const P2PParams p) {
   static_assert(!kAsync || (kLdsC && !kSpec && !kNet), "lane-asynchronous ticks: plain or sparse path, LDS cells");
   static_assert(!kWire || (!kSpec && !kSparse && !kNet && !kAsync), "packet-fed ticks: the plain lock-step path");
-  static_assert(!kLive || (!kLdsC && !kAsync && !kSpec && !kSparse && !kNet && p2p_lds_queue<G>()),
-                "one-tick launches: the plain and packet-fed paths of lane-per-player games with 1-byte inputs");
   using InRec = typename G::InRec;
   using CS = typename G::CS;
   constexpr int NW = G::NWL;
@@ -803,7 +758,7 @@ p2p_kernel(const P2PParams p) {
   // process would have aborted): it reports RB_PANIC from then on and its
   // state, cells and queues stay as the panic left them.  (Checked once the
   // session's state loads are issued, so they do not wait for this one.)
-  if constexpr (kLive && (RB_P2P_EXP & 32)) return;  // (attribution builds only)
+  if constexpr (RB_P2P_EXP & 32) return;  // (attribution builds only: the launch floor)
   const bool panicked = p.status[s] == kP2PStatusPanic;
   const unsigned Spad = static_cast<unsigned>(p.Spad), Gpad = Spad * L;
   const unsigned slot_words = static_cast<unsigned>(NW) * Gpad;
@@ -813,8 +768,7 @@ p2p_kernel(const P2PParams p) {
   const RingIO<IB> hbm{reinterpret_cast<uint8_t*>(p.ring), P, p.Spad};
   extern __shared__ uint8_t lds_queue[];
   const auto ring = [&]() __attribute__((always_inline)) {
-    if constexpr (kLive) return WinRing{hbm, 0, 0u, 0u, 0u, 0u, 0u};
-    else if constexpr (kLdsQ) return LdsRing{lds_queue + threadIdx.x, blockDim.x};
+    if constexpr (kLdsQ) return LdsRing{lds_queue + threadIdx.x, blockDim.x};
     else return hbm;
   }();
   // the in-kernel fan-out (the batch's branches are this kernel's own unless fan_generic)
@@ -850,9 +804,9 @@ p2p_kernel(const P2PParams p) {
       q[j].tail = *qrow(QF_TAIL, h);
       q[j].len = *qrow(QF_LEN, h);
       q[j].bad = false;
-      // the fan-out's candidate list, for an alphabet larger than K (launch-uniform)
-      q[j].mtf = kSpec && InputAlphabet<G>::value > static_cast<uint32_t>(p.fan_k);
-      if constexpr (kSpec) {
+      // the fan-out's candidate list, for an alphabet larger than K
+      q[j].mtf = kSpec && kMtf;
+      if constexpr (kSpec && kMtf) {
         q[j].mlo = static_cast<uint32_t>(*qrow(QF_MTF0, h)) | static_cast<uint64_t>(static_cast<uint32_t>(*qrow(QF_MTF0 + 1, h))) << 32;
         q[j].mhi = static_cast<uint32_t>(*qrow(QF_MTF0 + 2, h)) | static_cast<uint64_t>(static_cast<uint32_t>(*qrow(QF_MTF0 + 3, h))) << 32;
         q[j].mn = *qrow(QF_MTF_N, h);
@@ -928,7 +882,7 @@ p2p_kernel(const P2PParams p) {
     up[j] = load_upto(0, j);
     lin[j] = load_local(0, j);
   }
-  // kWire + kLive: the first tick's packets with them (length, start frame, first 32 bytes)
+  // kWire: a tick's packet (length, start frame, first 32 bytes)
   struct PkHead {
     int32_t n, start;
     uint32_t w0[8];
@@ -943,15 +897,6 @@ p2p_kernel(const P2PParams p) {
     r.w0[0] = a.x, r.w0[1] = a.y, r.w0[2] = a.z, r.w0[3] = a.w, r.w0[4] = b.x, r.w0[5] = b.y, r.w0[6] = b.z, r.w0[7] = b.w;
     return r;
   };
-  [[maybe_unused]] PkHead pk_live{0, 0, {}};
-  if constexpr (kWire && kLive) pk_live = wire_fetch(min(player_of(0), P - 1), 0);
-  // kLive: the work counters this launch adds to, loaded with the rest (an update at the end
-  // would load them after every store of the tick)
-  [[maybe_unused]] unsigned long long st_pre[4] = {0ull, 0ull, 0ull, 0ull};
-  if constexpr (kLive) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) st_pre[i] = p.stats[i * Spad + s];
-  }
   if (panicked) return;
   // LDS queue: the HBM frames this launch can read.  Reads are of frames
   // >= cur - W (adjust_gamestate checks that before it advances) up to the
@@ -1304,35 +1249,7 @@ p2p_kernel(const P2PParams p) {
 #pragma unroll
     for (int k = 0; k < kPre; ++k) rv[j][k] = load_remote(j, f + k);
   }
-  if constexpr (kLive && !(RB_P2P_EXP & 8)) {  // the input window (frames cur - W .. cur of this lane's player), issued after the deliveries
-    const int hw = min(player_of(0), P - 1);
-    ring.lo = cur - W;
-    uint32_t b[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) b[k] = hbm.get(max(ring.frame_of(static_cast<uint32_t>(k)), 0), hw, s);
-    ring.w0 = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
-    ring.w1 = b[4] | (b[5] << 8) | (b[6] << 16) | (b[7] << 24);
-    ring.w2 = b[8] | (b[9] << 8) | (b[10] << 16) | (b[11] << 24);
-    ring.w3 = b[12] | (b[13] << 8) | (b[14] << 16) | (b[15] << 24);
-    // Everything the tick reads before its LoadGameState is in flight now; consume it here, in
-    // the entry block.  Otherwise the compiler sinks each load into the conditional block of its
-    // first use (the remote player's poll, past the window's wait), which costs a round trip.
-#pragma unroll
-    for (int j = 0; j < PPL; ++j) {
-      settle(static_cast<uint32_t>(up[j]));
-      settle(lin[j]);
-#pragma unroll
-      for (int k = 0; k < kPre; ++k) settle(rv[j][k]);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) settle(static_cast<uint64_t>(st_pre[i]));
-    if constexpr (kWire) {
-      settle(static_cast<uint32_t>(pk_live.n));
-      settle(static_cast<uint32_t>(pk_live.start));
-#pragma unroll
-      for (int i = 0; i < 8; ++i) settle(pk_live.w0[i]);
-    }
-  }
+
 
   // ---- kWire: UdpProtocol::on_input (protocol.rs:616-689) for the endpoint
   // of remote handle h, fused into the poll.  The packet is the XOR delta of
@@ -1349,7 +1266,7 @@ p2p_kernel(const P2PParams p) {
       return kWireNothing;
     } else {
       const size_t idx = (static_cast<size_t>(t) * P + static_cast<size_t>(h)) * static_cast<size_t>(p.S) + s;
-      const PkHead hd = kLive ? pk_live : wire_fetch(h, t);  // (kLive: loaded at entry)
+      const PkHead hd = wire_fetch(h, t);
       const int32_t n = hd.n, start = hd.start;
       const uint8_t* pk = p.packets + static_cast<int64_t>(idx) * p.packet_stride;
       uint32_t w0[8];
@@ -1490,7 +1407,7 @@ p2p_kernel(const P2PParams p) {
   // The next tick's deliveries are prefetched, except by the P2P launches of
   // the two-launch fan-out (fanout_kernel), which are always of one tick (the
   // fan-out runs between ticks): there they would only hold registers.
-  constexpr bool kPrefetch = (!kSpec || kInFan) && !kLive;
+  constexpr bool kPrefetch = !kSpec || kInFan;
   auto tick_begin = [&](int t) __attribute__((always_inline)) -> int {
     const int tn = t + 1 < p.T ? t + 1 : t;
     if constexpr (kPrefetch) {
@@ -1690,7 +1607,7 @@ p2p_kernel(const P2PParams p) {
       // values gives a compile-time set.
       uint32_t cand[4];
       int nb;
-      if (InputAlphabet<G>::value <= static_cast<uint32_t>(p.fan_k)) {
+      if constexpr (!kMtf) {  // the whole alphabet (at most K values)
         constexpr auto AC = AlphabetClasses<G>::value;
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) cand[qq] = AC.packed[qq];
@@ -1828,9 +1745,7 @@ p2p_kernel(const P2PParams p) {
     tick_rotate();
     return true;
   };
-  if constexpr (kLive) {
-    if constexpr (!(RB_P2P_EXP & 24)) tick(0);  // (exactly one tick: no loop bound to branch on before the first use)
-  } else if constexpr (!kAsync) {
+  if constexpr (!kAsync) {
     for (int t = 0; t < p.T; ++t)
       if (!tick(t)) break;
   } else {
@@ -1905,14 +1820,6 @@ p2p_kernel(const P2PParams p) {
     }
   }
 
-  // ---- kLive: the window's frames put in this launch back to the HBM ring
-  if constexpr (kLive) {
-    const int hw = min(player_of(0), P - 1);
-    for (uint32_t d = ring.dirty; d; d &= d - 1) {
-      const uint32_t k = static_cast<uint32_t>(__builtin_ctz(d));
-      hbm.put(ring.frame_of(k), hw, s, ring.byte(k));
-    }
-  }
   // ---- LDS queue: the frames added in this launch back to the HBM ring
   if constexpr (kLdsQ) {
     const int h = player_of(0);
@@ -1949,8 +1856,8 @@ p2p_kernel(const P2PParams p) {
     *qrow(QF_TAIL, h) = q[j].tail;
     *qrow(QF_LEN, h) = q[j].len;
     if constexpr (kNet) *qrow(QF_DISC, h) = q[j].disc ? 1 : 0;  // update_player_disconnects may set it
-    if constexpr (kSpec) {
-      if (q[j].mtf) {
+    if constexpr (kSpec && kMtf) {
+      {
         *qrow(QF_MTF0, h) = static_cast<int32_t>(q[j].mlo);
         *qrow(QF_MTF0 + 1, h) = static_cast<int32_t>(q[j].mlo >> 32);
         *qrow(QF_MTF0 + 2, h) = static_cast<int32_t>(q[j].mhi);
@@ -1986,17 +1893,10 @@ p2p_kernel(const P2PParams p) {
     p.trace[TR_NSAVE * Spad + s] = nsave;
     if (status == kP2PStatusPanic) atomicAdd(&p.counters[2], 1u);
     if (n_thr) atomicAdd(&p.counters[0], n_thr);
-    if constexpr (kLive) {
-      p.stats[ST_ADV * Spad + s] = st_pre[ST_ADV] + tot_adv;
-      p.stats[ST_SAVE * Spad + s] = st_pre[ST_SAVE] + tot_save;
-      p.stats[ST_LOAD * Spad + s] = st_pre[ST_LOAD] + tot_load;
-      p.stats[ST_SELECT * Spad + s] = st_pre[ST_SELECT] + tot_sel;
-    } else {
-      p.stats[ST_ADV * Spad + s] += tot_adv;
-      p.stats[ST_SAVE * Spad + s] += tot_save;
-      p.stats[ST_LOAD * Spad + s] += tot_load;
-      p.stats[ST_SELECT * Spad + s] += tot_sel;
-    }
+    p.stats[ST_ADV * Spad + s] += tot_adv;
+    p.stats[ST_SAVE * Spad + s] += tot_save;
+    p.stats[ST_LOAD * Spad + s] += tot_load;
+    p.stats[ST_SELECT * Spad + s] += tot_sel;
     if constexpr (kInFan) {
       if (in_fan) {  // the branches' metadata for the next launch's first tick
         p.stats[ST_BRANCH * Spad + s] += tot_branch;

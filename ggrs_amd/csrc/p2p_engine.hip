@@ -29,7 +29,6 @@ struct rb_p2p {
   bool fanout = false;
   bool sync_ticks = false;   // RB_P2P_SYNC_TICKS=1 at create: lock-step ticks (p2p.hpp kAsync off)
   bool fan_generic = false;  // RB_FANOUT_GENERIC=1 at create: fanout_kernel for every game
-  bool live_tick = true;     // RB_P2P_LIVE=0 at create: one-tick launches without p2p_kernel kLive (A/B, tests)
   uint32_t* spec_state = nullptr;
   uint32_t* spec_cells = nullptr;
   void* spec_cs = nullptr;
@@ -238,7 +237,6 @@ rb_status rb_p2p_create(const rb_p2p_config* cfg, rb_p2p** out) {
   b->fanout = fanout;
   if (const char* e = std::getenv("RB_P2P_SYNC_TICKS")) b->sync_ticks = std::atoi(e) != 0;
   if (const char* e = std::getenv("RB_FANOUT_GENERIC")) b->fan_generic = std::atoi(e) != 0;
-  if (const char* e = std::getenv("RB_P2P_LIVE")) b->live_tick = std::atoi(e) != 0;
   rb_p2p* bp = b.get();
   auto hip_fail = [&](hipError_t e, const char* what) {
     g_p2p_err = std::string(what) + ": " + hipGetErrorString(e);
@@ -387,7 +385,6 @@ P2PParams base_params(const rb_p2p* b) {
   p.local_mask = b->cfg.local_mask;
   p.sparse = b->cfg.sparse_saving != 0;
   p.sync_ticks = b->sync_ticks ? 1 : 0;
-  p.live_tick = b->live_tick ? 1 : 0;
   p.fan_generic = b->fan_generic ? 1 : 0;
   p.fan_k = b->cfg.fanout_candidates;
   p.spec_on = b->fanout ? 1 : 0;
@@ -443,12 +440,14 @@ rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs,
     e0 = b->prof_ev[b->prof_used].first;
     e1 = b->prof_ev[b->prof_used].second;
     ++b->prof_used;
-    P2P_TRY(b, hipEventRecord(e0, b->stream));
   }
+  const bool one_launch = !b->fanout || (b->ops->inlane_fanout && !b->fan_generic);
   hipError_t e = hipSuccess;
-  if (!b->fanout || (b->ops->inlane_fanout && !b->fan_generic)) {
-    e = b->ops->launch_p2p(p, b->block, b->stream);  // all ticks in one launch (with the in-kernel fan-out)
+  if (one_launch) {
+    // all ticks in one launch (with the in-kernel fan-out); timed by the kernel's own start / end
+    e = b->ops->launch_p2p(p, b->block, b->stream, LaunchEv{e0, e1});
   } else {
+    if (e0) P2P_TRY(b, hipEventRecord(e0, b->stream));
     // fanout_kernel between ticks needs every lane of a session's branches: one
     // P2P launch and one fan-out launch per tick
     P2PParams pt = p;
@@ -461,7 +460,7 @@ rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs,
     }
   }
   if (e != hipSuccess) return pfail(b, RB_DEVICE_ERROR, std::string("p2p launch: ") + hipGetErrorString(e));
-  if (b->prof) P2P_TRY(b, hipEventRecord(e1, b->stream));
+  if (e1 && !one_launch) P2P_TRY(b, hipEventRecord(e1, b->stream));
   return RB_OK;
 }
 
@@ -492,7 +491,7 @@ rb_status rb_p2p_run_ticks_packets(rb_p2p* b, int32_t n_ticks, const void* local
   p.pk_status = decode_status;
   p.acks = acks;
   P2P_TRY(b, hipSetDevice(b->device));
-  hipEvent_t e1 = nullptr;
+  LaunchEv ev;  // the kernel's own start / end (hipExtLaunchKernel)
   if (b->prof) {
     if (b->prof_used == b->prof_ev.size()) {
       hipEvent_t e0 = nullptr, e2 = nullptr;
@@ -500,13 +499,11 @@ rb_status rb_p2p_run_ticks_packets(rb_p2p* b, int32_t n_ticks, const void* local
       P2P_TRY(b, hipEventCreate(&e2));
       b->prof_ev.emplace_back(e0, e2);
     }
-    P2P_TRY(b, hipEventRecord(b->prof_ev[b->prof_used].first, b->stream));
-    e1 = b->prof_ev[b->prof_used].second;
+    ev = LaunchEv{b->prof_ev[b->prof_used].first, b->prof_ev[b->prof_used].second};
     ++b->prof_used;
   }
-  hipError_t e = b->ops->launch_p2p(p, b->block, b->stream);
+  hipError_t e = b->ops->launch_p2p(p, b->block, b->stream, ev);
   if (e != hipSuccess) return pfail(b, RB_DEVICE_ERROR, std::string("p2p launch: ") + hipGetErrorString(e));
-  if (e1) P2P_TRY(b, hipEventRecord(e1, b->stream));
   return RB_OK;
 }
 

@@ -2,7 +2,7 @@
 bench lines time, at 65,536 sessions — plain rollback (lane-asynchronous ticks
 over the LDS snapshot ring, 50 ticks per launch), sparse saving, the C4
 speculative fan-out (P = 4, K = 16), packet-fed replay and one-tick launches
-(live play, p2p_kernel kLive) — each checked two ways:
+(live play) — each checked two ways:
 
 * size-independent properties of the whole batch: no panic; the fan-out's
   cells, states and queues equal a plain rollback batch's on the same inputs
@@ -115,8 +115,9 @@ def test_gpu_p2p_bench_path_at_full_size(gpu_available, sparse):
 
 
 def test_gpu_p2p_one_tick_launches_at_full_size(gpu_available):
-    """Live play (one launch per tick: p2p_kernel kLive, the input window in registers) at
-    65,536 sessions equals the fused 50-tick launches bit for bit, and the oracle sample."""
+    """Live play (one launch per tick, the cells and the input ring in HBM) at 65,536 sessions
+    equals the fused 50-tick launches (LDS rings, lane-asynchronous ticks) bit for bit, and the
+    oracle sample."""
     P, T = 2, 60
     (inputs, upto, rin), (di, du, dr) = network(P, T)
     live, fused = batch(P), batch(P)
