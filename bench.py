@@ -822,8 +822,11 @@ def main():
         else:
             model = "algorithmic (SURVEY 8d): 1 load + cd saves x 40 B, checksums, inputs, status"
         bytes_per_launch = bpt * (S + A) * ticks_per_launch  # the kernel runs the audit replicas too
+        # the PMC profile of exactly the launch shape timed here: ticks per timed launch (the driver's
+        # --steps 20 times one 20-tick launch, whatever --ticks-per-launch says)
+        tl = int(round(ticks_per_launch))
         cfg_key = f"{args.game} P={P} cd={cd} W={args.max_prediction} d={args.input_delay} S={S}" + (
-            f" tpl={tpl}" if tpl != 50 else "")
+            f" tpl={tl}" if tl != 50 else "")
         roofline = roofline_block(bytes_per_launch, avg_kernel_s, ticks_per_launch, launches,
                                   ((f"steady_kernel<Brawler<{P}>,{cd}>" if brawler else
                                     f"steady_kernel<ExGame<{P},true>,{cd}>") +

@@ -147,6 +147,7 @@ struct rb_batch {
   // call fails with RB_PANIC, as the reference process would have stopped.
   std::string poisoned;
   bool pipe = false;  // fused steady ticks with two ticks in flight (RB_STEADY_PIPE=1 at create; A/B, tests)
+  uint32_t lds_pad = 0;  // RB_LDS_PAD (bytes) at create: dynamic LDS reserved per steady workgroup (A/B)
 };
 
 namespace {
@@ -334,6 +335,7 @@ rb_status rb_synctest_create(const rb_config* cfg, rb_batch** out) {
   b->W = cfg->max_prediction;
   b->P = cfg->num_players;
   b->block = cfg->block_size ? static_cast<int>(cfg->block_size) : 256;
+  if (const char* env = std::getenv("RB_LDS_PAD")) b->lds_pad = static_cast<uint32_t>(std::atoi(env));
 #if RB_EXPERIMENTS  // steady_pipe_kernel exists in A/B builds only
   if (const char* env = std::getenv("RB_STEADY_PIPE")) b->pipe = std::atoi(env) != 0;
 #endif
@@ -555,6 +557,7 @@ rb_status launch_steady_run(rb_batch* b, const uint8_t* tick_inputs, int64_t str
   r.seed = b->cfg.seed;
   r.debug = b->cfg.reserved[0];
   r.pipe = b->pipe ? 1 : 0;
+  r.lds_pad = b->lds_pad;
   const bool timed = b->prof;
   LaunchEv ev;  // the kernel's own start / end (hipExtLaunchKernel), no marker packets around it
   if (timed) {

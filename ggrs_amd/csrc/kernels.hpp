@@ -338,6 +338,7 @@ struct RunParams {
   uint64_t seed;
   uint32_t debug;           // experiment knobs (rb_config.reserved[0]); 0 in every real run
   int32_t pipe;             // 1: two ticks in flight per lane where the game allows it (steady_pipe.hpp)
+  uint32_t lds_pad;         // dynamic LDS bytes per workgroup the launch reserves (unused: caps workgroups per CU)
 };
 
 // An empty asm that reads v: the compiler must complete the load that
@@ -385,8 +386,15 @@ using DecOf = typename DecSel<G>::type;
 
 // kExp: attribution experiments (RunParams::debug knobs, tools/exp_steady.py);
 // instantiated only in builds made with RB_EXPERIMENTS=1, never in the product.
+#ifndef RB_STEADY_WAVES_PER_EU
+#define RB_STEADY_WAVES_PER_EU 0  // >0: the occupancy the compiler may schedule for (A/B builds)
+#endif
 template <class G, int CD, bool kExp>
-__global__ void __launch_bounds__(256) steady_kernel(const RunParams p) {
+__global__ void __launch_bounds__(256)
+#if RB_STEADY_WAVES_PER_EU > 0
+__attribute__((amdgpu_waves_per_eu(1, RB_STEADY_WAVES_PER_EU)))
+#endif
+steady_kernel(const RunParams p) {
   static_assert(CD >= 1, "steady shape needs a rollback");
   const uint32_t dbg = kExp ? p.debug : 0u;
   using InRec = typename G::InRec;
@@ -731,7 +739,7 @@ struct GameOpsT final : GameOps {
       }
     }
 #endif
-    return rb_launch(steady_kernel<G, CD, false>, dim3(grid), dim3(block), 0, st, ev, p);
+    return rb_launch(steady_kernel<G, CD, false>, dim3(grid), dim3(block), p.lds_pad, st, ev, p);
   }
   hipError_t launch_steady(const RunParams& p, int cd, int block, hipStream_t st, const LaunchEv& ev) const override {
     switch (cd) {
