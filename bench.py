@@ -515,7 +515,8 @@ def bench_p2p(args):
                        "rollbacks_per_session_tick": (loads + selects) / (S * world * args.steps),
                        "speculative": ({"branches": K, "alphabet": 16 if not brawler else 256,
                                         "candidates": "whole alphabet" if (not brawler and K >= 16) else
-                                                      "K most recently confirmed distinct inputs, then smallest values",
+                                                      "the K most recently added distinct inputs (the queue's "
+                                                      "move-to-front list), then the smallest values",
                                         "selects": selects, "loads": loads,
                                         "select_fraction": selects / max(1, selects + loads),
                                         "branch_frames_per_s": branch / elapsed}

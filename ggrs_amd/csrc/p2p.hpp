@@ -901,9 +901,9 @@ p2p_kernel(const P2PParams p) {
   // LDS queue: the HBM frames this launch can read.  Reads are of frames
   // >= cur - W (adjust_gamestate checks that before it advances) up to the
   // last added one, or of the last added frame itself (predictions and the
-  // delay replication); every later frame is added inside the launch.  The
-  // in-kernel fan-out choosing K of a larger alphabet also reads the 32 frames
-  // up to the last added one (fan_candidates).
+  // delay replication); every later frame is added inside the launch.  (The
+  // fan-out's candidates come from the queue's move-to-front list, not from
+  // these frames: fan_candidates.)
   const int32_t la0 = q[0].last_added;
   if constexpr (kLdsQ) {
     const int h = player_of(0);
