@@ -487,6 +487,8 @@ def bench_p2p(args):
         cfg_key = (f"p2p {args.game} P={P} W={W} d={args.input_delay} rd={args.remote_delay} lag={lo},{hi} S={S}"
                    + (" sparse" if args.sparse_saving else "") + (f" fanout{'' if K == 16 else K}" if args.fanout else "")
                    + (" wire" if args.wire else "") + (" wire-replay" if args.wire_replay else ""))
+        tl = int(round(args.steps / max(1, launches)))  # the PMC profile of the launch shape timed here
+        cfg_key += f" tpl={tl}" if tl != 50 else ""
         gname = f"Brawler<{P}>" if brawler else f"ExGame<{P},true>"
         roofline = roofline_block(bytes_rank / max(1, launches), avg_kernel_s, args.steps / max(1, launches), launches,
                                   f"p2p_kernel<{gname}>" + ((" + fanout_kernel (per tick)" if generic_fan or brawler
