@@ -100,15 +100,19 @@ struct InputAlphabet<G, std::void_t<decltype(G::kInputAlphabet)>> {
 // its 16 most recent distinct inputs, updated as each input is added (mtf_push),
 // so picking the candidates reads no input history — then, while the queue has
 // seen fewer than K distinct values, the smallest values not yet taken.  Packed
-// 4 per word, unused slots 0xFF.
+// 4 per word, unused slots 0xFF.  For the in-kernel fan-out, whose branches are
+// input classes (InputCanon), the list holds classes (DevQueue::mcanon) and the
+// fill takes only class representatives (`allowed`): ex_game's K = 8 then
+// covers 8 of its 9 classes instead of the classes of 8 raw inputs.
 // The fill of fan_candidates: the smallest values of the alphabet not among the first `take` list
 // entries, into list slots take .. K-1.  Out of line: it runs only while a queue has seen fewer
 // than K distinct inputs, and its bitmaps would otherwise hold registers in the fan-out kernels.
 struct CandList {
   uint64_t lo, hi;
 };
-__device__ __noinline__ CandList fan_fill(uint64_t lo, uint64_t hi, int take, uint32_t alphabet, int K) {
-  uint64_t present[4] = {0ull, 0ull, 0ull, 0ull};
+__device__ __noinline__ CandList fan_fill(uint64_t lo, uint64_t hi, int take, uint32_t alphabet, int K,
+                                         uint64_t allowed) {
+  uint64_t present[4] = {~allowed, 0ull, 0ull, 0ull};  // values never filled count as taken
   for (int i = 0; i < take; ++i) {
     const uint32_t v = static_cast<uint32_t>((i < 8 ? lo >> (8 * i) : hi >> (8 * (i - 8))) & 0xFFull);
     present[v >> 6] |= 1ull << (v & 63);
@@ -126,7 +130,7 @@ __device__ __noinline__ CandList fan_fill(uint64_t lo, uint64_t hi, int take, ui
   return CandList{lo, hi};
 }
 __device__ __forceinline__ void fan_candidates(uint64_t mlo, uint64_t mhi, int32_t mn, uint32_t alphabet, int K,
-                                               uint32_t (&packed)[4]) {
+                                               uint32_t (&packed)[4], uint64_t allowed = ~0ull) {
   if (alphabet <= static_cast<uint32_t>(K)) {
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
@@ -145,7 +149,7 @@ __device__ __forceinline__ void fan_candidates(uint64_t mlo, uint64_t mhi, int32
   const uint64_t khi = take <= 8 ? 0ull : (take >= 16 ? ~0ull : ((1ull << (8 * (take - 8))) - 1ull));
   uint64_t lo = (mlo & klo) | ~klo, hi = (mhi & khi) | ~khi;
   if (take < K) {  // a queue that has seen fewer than K distinct inputs
-    const CandList c = fan_fill(lo, hi, take, alphabet, K);
+    const CandList c = fan_fill(lo, hi, take, alphabet, K, allowed);
     lo = c.lo;
     hi = c.hi;
   }
@@ -241,6 +245,14 @@ struct AlphabetClasses {
   }
   static constexpr T value = make();
 };
+// The values v < 64 that represent their class (canon(v) == v): what the fill of a class list
+// may add (every value for a game without classes).
+template <class G>
+constexpr uint64_t canon_reps() {
+  uint64_t m = 0;
+  for (uint32_t v = 0; v < 64; ++v) m |= (InputCanon<G>::apply(v) == v) ? 1ull << v : 0ull;
+  return m;
+}
 // The classes of the first K packed candidates, deduplicated in candidate
 // order (the branches of the in-kernel fan-out); returns their count.
 template <class G>
@@ -494,8 +506,10 @@ struct DevQueue {
   bool bad;
   int32_t tail, len;
   // the fan-out's move-to-front list of the most recent distinct inputs (fan_candidates), kept
-  // only by fan-out batches whose alphabet is larger than K (mtf); bytes 0-7 / 8-15 newest first
-  bool mtf;
+  // only by fan-out batches whose alphabet is larger than K (mtf); bytes 0-7 / 8-15 newest first.
+  // mcanon: the list holds input classes (InputCanon), for the in-kernel fan-out, whose branches
+  // are classes: K recent classes cover more of the moves than K recent raw inputs
+  bool mtf, mcanon;
   uint64_t mlo, mhi;
   int32_t mn;
 };
@@ -610,11 +624,11 @@ constexpr bool p2p_lds_cells(int W, int block) {
          p2p_lds_bytes<G, true>(block) + p2p_lds_cell_bytes<G>(block, W) <= kLdsPerBlockMax;
 }
 
-// input_queue.rs:167-204 add_input_by_frame
-template <class R>
+// input_queue.rs:167-204 add_input_by_frame (Cn: the game's InputCanon, for the fan-out's list)
+template <class Cn, class R>
 __device__ __forceinline__ void q_add_by_frame(DevQueue& q, const R& r, int h, unsigned s, int32_t f, uint32_t v) {
   r.put(f, h, s, v);
-  if (q.mtf) mtf_push(q, v);
+  if (q.mtf) mtf_push(q, q.mcanon ? Cn::apply(v) : v);
   q.last_added = f;
   q.len += 1;
   // the prediction bookkeeping as selects (no branch: every call site is in the hot poll)
@@ -625,15 +639,15 @@ __device__ __forceinline__ void q_add_by_frame(DevQueue& q, const R& r, int h, u
 }
 // input_queue.rs:149-163 + 207-239 add_input with the delay already applied to
 // `f`: replicate the entry before head (blank before the first add) up to f.
-template <class R>
+template <class Cn, class R>
 __device__ __forceinline__ int32_t q_add(DevQueue& q, const R& r, int h, unsigned s, int32_t f, uint32_t v) {
   int32_t expected = q.last_added == kNullFrame ? 0 : q.last_added + 1;
   if (expected > f) return kNullFrame;
   if (expected < f) {  // only a queue's first add replicates (the input-delay fill)
     const uint32_t rep = q.last_added == kNullFrame ? 0u : r.get(q.last_added, h, s);
-    for (; expected < f; ++expected) q_add_by_frame(q, r, h, s, expected, rep);
+    for (; expected < f; ++expected) q_add_by_frame<Cn>(q, r, h, s, expected, rep);
   }
-  q_add_by_frame(q, r, h, s, f, v);
+  q_add_by_frame<Cn>(q, r, h, s, f, v);
   return f;
 }
 // input_queue.rs:83-101 discard_confirmed_frames(frame).  "Delete all but the
@@ -806,6 +820,7 @@ p2p_kernel(const P2PParams p) {
       q[j].bad = false;
       // the fan-out's candidate list, for an alphabet larger than K
       q[j].mtf = kSpec && kMtf;
+      q[j].mcanon = kSpec && kMtf && InputCanon<G>::value && in_fan;  // the in-kernel fan-out: classes
       if constexpr (kSpec && kMtf) {
         q[j].mlo = static_cast<uint32_t>(*qrow(QF_MTF0, h)) | static_cast<uint64_t>(static_cast<uint32_t>(*qrow(QF_MTF0 + 1, h))) << 32;
         q[j].mhi = static_cast<uint32_t>(*qrow(QF_MTF0 + 2, h)) | static_cast<uint64_t>(static_cast<uint32_t>(*qrow(QF_MTF0 + 3, h))) << 32;
@@ -1305,7 +1320,7 @@ p2p_kernel(const P2PParams p) {
             if (i == IB - 1) {
               const int32_t f = start + k / IB;
               if (f > last) {  // protocol.rs:661-663
-                q_add(q[j], ring, h, s, f, acc);
+                q_add<InputCanon<G>>(q[j], ring, h, s, f, acc);
                 q[j].conn_last = f;
               }
               acc = 0;
@@ -1336,7 +1351,7 @@ p2p_kernel(const P2PParams p) {
           if (i == IB - 1) {
             const int32_t f = start + k / IB;
             if (f > last) {  // protocol.rs:661-663: inputs already received are skipped
-              q_add(q[j], ring, h, s, f, acc);  // add_remote_input (frame delay 0)
+              q_add<InputCanon<G>>(q[j], ring, h, s, f, acc);  // add_remote_input (frame delay 0)
               q[j].conn_last = f;
             }
             acc = 0;
@@ -1439,11 +1454,11 @@ p2p_kernel(const P2PParams p) {
 #pragma unroll
         for (int k = 0; k < kPre; ++k, ++f) {
           if (f > end) break;
-          q_add(q[j], ring, h, s, f, rv[j][k]);  // add_remote_input (frame delay 0)
+          q_add<InputCanon<G>>(q[j], ring, h, s, f, rv[j][k]);  // add_remote_input (frame delay 0)
           q[j].conn_last = f;
         }
         for (; f <= end; ++f) {  // more than kPre frames delivered in one tick
-          q_add(q[j], ring, h, s, f, load_remote(j, f));
+          q_add<InputCanon<G>>(q[j], ring, h, s, f, load_remote(j, f));
           q[j].conn_last = f;
         }
       }
@@ -1573,7 +1588,7 @@ p2p_kernel(const P2PParams p) {
     for (int j = 0; j < PPL; ++j) {
       const int h = player_of(j);
       if (h >= P || !((p.local_mask >> h) & 1u)) continue;
-      q[j].conn_last = q_add(q[j], ring, h, s, cur + p.delay, lin[j]);  // local_connect_status[h].last_frame
+      q[j].conn_last = q_add<InputCanon<G>>(q[j], ring, h, s, cur + p.delay, lin[j]);  // local_connect_status[h].last_frame
     }
   };
   // ---- the in-kernel fan-out (kInFan, see inlane_fan), after the tick: the
@@ -1602,9 +1617,9 @@ p2p_kernel(const P2PParams p) {
       const unsigned bslot = static_cast<unsigned>(base >= 0 ? base % W : 0);
       const int32_t btag = kLdsC ? lds_tag[bslot * bps + sl] : p.tag[bslot * Spad + s];
       const bool valid = !(RB_FAN_EXP & 1) && !any_disc && rs >= 0 && base < cur && base + W > cur && base >= 0 && btag == base;
-      // the speculated player's candidates, from its queue's ring (every lane reads the same column),
-      // as their distinct classes (InputCanon): one branch per class.  A whole alphabet of at most K
-      // values gives a compile-time set.
+      // the speculated player's candidates as distinct classes (InputCanon): one branch per class.
+      // A whole alphabet of at most K values gives a compile-time set; otherwise the queue's
+      // move-to-front list, which for this fan-out already holds distinct classes (mcanon).
       uint32_t cand[4];
       int nb;
       if constexpr (!kMtf) {  // the whole alphabet (at most K values)
@@ -1618,9 +1633,15 @@ p2p_kernel(const P2PParams p) {
                              static_cast<uint64_t>(static_cast<uint32_t>(__shfl(static_cast<int>(q[0].mlo >> 32), src, 64))) << 32;
         const uint64_t mhi = static_cast<uint32_t>(__shfl(static_cast<int>(q[0].mhi), src, 64)) |
                              static_cast<uint64_t>(static_cast<uint32_t>(__shfl(static_cast<int>(q[0].mhi >> 32), src, 64))) << 32;
-        uint32_t raw[4];
-        fan_candidates(mlo, mhi, __shfl(q[0].mn, src, 64), InputAlphabet<G>::value, p.fan_k, raw);
-        nb = cand_classes<G>(raw, p.fan_k, cand);
+        fan_candidates(mlo, mhi, __shfl(q[0].mn, src, 64), InputAlphabet<G>::value, p.fan_k, cand, canon_reps<G>());
+        // distinct classes in a prefix, unused slots 0xFF after it: the branch count is the index
+        // of the first 0xFF byte (the lowest zero byte of the complement, exact)
+        const uint64_t xl = ~(static_cast<uint64_t>(cand[1]) << 32 | cand[0]);
+        const uint64_t xh = ~(static_cast<uint64_t>(cand[3]) << 32 | cand[2]);
+        const uint64_t zl = (xl - 0x0101010101010101ull) & ~xl & 0x8080808080808080ull;
+        const uint64_t zh = (xh - 0x0101010101010101ull) & ~xh & 0x8080808080808080ull;
+        nb = min(p.fan_k, zl ? static_cast<int>(__builtin_ctzll(zl) >> 3)
+                             : (zh ? 8 + static_cast<int>(__builtin_ctzll(zh) >> 3) : kSpecBranches));
       }
       sm_valid = valid ? (1 | (nb << 8)) : 0;  // (the branch count rides along)
       sm_base = base;
@@ -1671,13 +1692,15 @@ p2p_kernel(const P2PParams p) {
         }
         advance_frame<G>(x, in, pl, 0u, &p.counters[1]);
       };
+      // One group of a lane's branch chains (NG of them advanced together: independent chains,
+      // instruction-level parallelism), b0 = the group's first branch slot of this lane.
+      auto group = [&](auto ng_tag, int b0) __attribute__((always_inline)) {
+        constexpr int NG = decltype(ng_tag)::value;
+        uint32_t wb[NG][NW];
+        InRec in[NG];
+        bool on[NG];
 #pragma unroll
-      for (int b0 = 0; b0 < kB; b0 += kFanGroup) {
-        uint32_t wb[kFanGroup][NW];
-        InRec in[kFanGroup];
-        bool on[kFanGroup];
-#pragma unroll
-        for (int b = 0; b < kFanGroup; ++b) {
+        for (int b = 0; b < NG; ++b) {
           const int k = (b0 + b) * L + krot;
           on[b] = k < nb;
           in[b] = static_cast<InRec>(static_cast<uint64_t>(cand_at(cand, k)) << (8 * rs));
@@ -1689,14 +1712,14 @@ p2p_kernel(const P2PParams p) {
           if (f > base && !(RB_FAN_EXP & 2)) {  // SaveGameState of frame f in every branch
             const unsigned slot = static_cast<unsigned>(f % W);
 #pragma unroll
-            for (int b = 0; b < kFanGroup; ++b)
+            for (int b = 0; b < NG; ++b)
               if (on[b])
                 store_words<NW>(p.spec_cells + slot * NW * Gs, static_cast<int>(Gs),
                                 static_cast<int>(s * kSpecBranches + static_cast<unsigned>((b0 + b) * L + krot)), wb[b]);
             if (run_own) store_words<NW>(p.spec_cells + slot * NW * Gs, static_cast<int>(Gs), static_cast<int>(ocol), ow);
           }
 #pragma unroll
-          for (int b = 0; b < kFanGroup; ++b) adv(wb[b], in[b], rs);
+          for (int b = 0; b < NG; ++b) adv(wb[b], in[b], rs);
           if (run_own) {
             const int j = f - base;
             uint32_t v;
@@ -1708,10 +1731,30 @@ p2p_kernel(const P2PParams p) {
         }
         if (run_own) store_words<NW>(p.spec_state, static_cast<int>(Gs), static_cast<int>(ocol), ow);
 #pragma unroll
-        for (int b = 0; b < kFanGroup; ++b)
+        for (int b = 0; b < NG; ++b)
           if (on[b])
             store_words<NW>(p.spec_state, static_cast<int>(Gs),
                             static_cast<int>(s * kSpecBranches + static_cast<unsigned>((b0 + b) * L + krot)), wb[b]);
+      };
+      // Only the chains some lane of the wave needs: branch slot b0 + b of lane krot is branch
+      // (b0 + b) * L + krot, needed when below the session's branch count (ex_game's 9 classes at
+      // P = 4: 3 chains per lane, not kFanGroup = 4; K = 8: 2).  Known at compile time for a
+      // whole-alphabet candidate set, a wave vote otherwise.
+#pragma unroll
+      for (int b0 = 0; b0 < kB; b0 += kFanGroup) {
+        int ng = 0;
+        if constexpr (!kMtf) {
+          constexpr int n = AlphabetClasses<G>::value.n;
+          ng = min(kFanGroup, max(0, (n - b0 * static_cast<int>(L) + static_cast<int>(L) - 1) / static_cast<int>(L)));
+        } else {
+#pragma unroll
+          for (int b = 0; b < kFanGroup; ++b) ng += __any((b0 + b) * static_cast<int>(L) + krot < nb) ? 1 : 0;
+        }
+        if (ng == 0 && b0 > 0) break;  // (group 0 also runs the other players' chains)
+        if (ng <= 1) group(std::integral_constant<int, 1>{}, b0);
+        else if (ng == 2) group(std::integral_constant<int, 2>{}, b0);
+        else if (ng == 3) group(std::integral_constant<int, 3>{}, b0);
+        else group(std::integral_constant<int, 4>{}, b0);
       }
       tot_branch += static_cast<uint32_t>(cur - base) * static_cast<uint32_t>(nb);
     }

@@ -10,6 +10,7 @@ case "${PART:-1}" in
 1)
   p driver "--ticks-per-launch 20" 20 20 &&
   p synctest "" 400 50 &&
+  p synctest1 "--ticks-per-launch 1" 100 50 &&
   p p2p "--session p2p" 400 50 &&
   p p2p1 "--session p2p --ticks-per-launch 1" 200 50 &&
   p p2p_sparse "--session p2p --sparse-saving" 400 50 ;;

@@ -14,6 +14,7 @@ f() {  # f <name> <config key> <ticks per launch>
 }
 f driver "$X tpl=20" 20
 f synctest "$X" 50
+f synctest1 "$X tpl=1" 1
 f p2p "$Q" 50
 f p2p1 "$Q tpl=1" 1
 f p2p_sparse "$Q sparse" 50
