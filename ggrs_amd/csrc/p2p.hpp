@@ -253,25 +253,6 @@ constexpr uint64_t canon_reps() {
   for (uint32_t v = 0; v < 64; ++v) m |= (InputCanon<G>::apply(v) == v) ? 1ull << v : 0ull;
   return m;
 }
-// The classes of the first K packed candidates, deduplicated in candidate
-// order (the branches of the in-kernel fan-out); returns their count.
-template <class G>
-__device__ __forceinline__ int cand_classes(const uint32_t (&cand)[4], int K, uint32_t (&cls)[4]) {
-#pragma unroll
-  for (int q = 0; q < 4; ++q) cls[q] = ~0u;
-  int n = 0;
-#pragma unroll
-  for (int i = 0; i < kSpecBranches; ++i) {
-    const uint32_t c = InputCanon<G>::apply(cand_at(cand, i)) & 0xFFu;
-    if (i < K && cand_find(cls, c, n) < 0) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        cls[q] = (n >> 2) == q ? ((cls[q] & ~(0xFFu << (8 * (n & 3)))) | (c << (8 * (n & 3)))) : cls[q];
-      ++n;
-    }
-  }
-  return n;
-}
 
 // ---------------------------------------------------------------------------
 // Desync detection (p2p_session.rs:154-157, 313-316, 873-928; the UdpProtocol
@@ -1111,13 +1092,13 @@ p2p_kernel(const P2PParams p) {
     exec = true;
     if (status == kP2PStatusPanic) return true;
     if (in_fan) {
-      // the in-kernel fan-out's branch kk: column s * 16 + kk, written by lane kk % L (which alone reads
+      // the in-kernel fan-out's branch kk: column s * 16 + kk, written by lane (rs + kk) % L (which alone reads
       // it back and hands the words to the speculated player's lane); every other lane keeps its own
       // cells and state (no misprediction of its player), and each cell's checksum is rebuilt from the
       // players' fletcher parts
       if constexpr (kInFan) {
         const unsigned Gs = Spad * static_cast<unsigned>(kSpecBranches + L);
-        const int owner = kk % L;  // (fan_inlane's branch-to-lane map)
+        const int owner = (rs + kk) % static_cast<int>(L);  // (fan_inlane's deal of branches to lanes)
         const unsigned col = s * kSpecBranches + static_cast<unsigned>(kk);
         const unsigned ocol = Spad * kSpecBranches + s * L + static_cast<unsigned>(lane);  // this lane's player, once
         const bool other = lane < P && lane != rs;
@@ -1662,11 +1643,16 @@ p2p_kernel(const P2PParams p) {
         load_words<NW>(p.snap + bslot * slot_words, static_cast<int>(Gpad), static_cast<int>(g) - lane + rs, bw);
         load_words<NW>(p.snap + bslot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), ow);
       }
-      // Every other player is simulated once from the base cell with the inputs a rollback would
-      // give it (confirmed, or the repeat-last prediction): not always the main trajectory's, which
-      // keeps the effect of predictions a PredictionThreshold tick dropped the rollback of
-      // (p2p_session.rs:320).  Its lane runs it next to its first branch group, into column
-      // Spad * 16 + s * L + lane.
+      // The chains: the nb branches and, in every other player's lane, that player simulated once
+      // from the base cell with the inputs a rollback would give it (confirmed, or the repeat-last
+      // prediction): not always the main trajectory's, which keeps the effect of predictions a
+      // PredictionThreshold tick dropped the rollback of (p2p_session.rs:320); into column
+      // Spad * 16 + s * L + lane.  Chain slots are dealt round-robin starting at the speculated
+      // player's lane, which simulates no player of its own: branch k runs in lane (rs + k) % L,
+      // slot k / L, and each other player's chain takes the wave's last slot, which no other
+      // player's lane needs for a branch.  So the wave runs ceil((nb + P - 1) / L) slots or fewer
+      // (ex_game's 9 classes at P = 4: 3, where branches by k % L plus the other players' chains
+      // took 4).
       const int h_own = min(lane, P - 1);  // (the padding lane of P = 3 reads a real row, unused)
       const bool other = lane < P && lane != rs;
       const bool own_local = (p.local_mask >> h_own) & 1u;
@@ -1677,8 +1663,10 @@ p2p_kernel(const P2PParams p) {
       const uint64_t vpk = fan_pack(vin);
       const unsigned Gs = Spad * static_cast<unsigned>(kSpecBranches + L);  // branch columns, then the others'
       const unsigned ocol = Spad * kSpecBranches + s * L + static_cast<unsigned>(lane);
-      constexpr int kB = kSpecBranches / L;  // branches per lane
-      const int krot = lane;  // branch k runs in lane k % L
+      const int r = (lane - rs) & static_cast<int>(L - 1);  // this lane's place in the deal
+      const int nbr = nb > r ? (nb - r + static_cast<int>(L) - 1) / static_cast<int>(L) : 0;  // its branch slots
+      // (an other player's lane has nbr < the wave's slot count: its own chain needs one more)
+      const int nslots = nbr + (other ? 1 : 0);
       // every chain of the wave starts in range (games.hpp in_range: e.g. ex_game rotations in [+0, 6.5),
       // which stay there for any number of frames): the AdvanceFrames skip the out-of-range library paths
       bool inr = false;
@@ -1692,69 +1680,64 @@ p2p_kernel(const P2PParams p) {
         }
         advance_frame<G>(x, in, pl, 0u, &p.counters[1]);
       };
-      // One group of a lane's branch chains (NG of them advanced together: independent chains,
-      // instruction-level parallelism), b0 = the group's first branch slot of this lane.
-      auto group = [&](auto ng_tag, int b0) __attribute__((always_inline)) {
+      // One group of a lane's chain slots b0 .. b0 + NG - 1, advanced together (independent chains:
+      // instruction-level parallelism); last: the group ends with the wave's last slot.
+      auto group = [&](auto ng_tag, int b0, bool last) __attribute__((always_inline)) {
         constexpr int NG = decltype(ng_tag)::value;
         uint32_t wb[NG][NW];
         InRec in[NG];
-        bool on[NG];
+        bool on[NG], own[NG];
+        unsigned col[NG];
+        bool any_own = false;
 #pragma unroll
         for (int b = 0; b < NG; ++b) {
-          const int k = (b0 + b) * L + krot;
+          const int sb = b0 + b;
+          const int k = sb * static_cast<int>(L) + r;
           on[b] = k < nb;
-          in[b] = static_cast<InRec>(static_cast<uint64_t>(cand_at(cand, k)) << (8 * rs));
+          own[b] = b == NG - 1 && last && other;
+          any_own |= own[b];
+          in[b] = static_cast<InRec>(static_cast<uint64_t>(cand_at(cand, k & (kSpecBranches - 1))) << (8 * rs));
+          col[b] = own[b] ? ocol : s * kSpecBranches + static_cast<unsigned>(k & (kSpecBranches - 1));
 #pragma unroll
-          for (int n = 0; n < NW; ++n) wb[b][n] = bw[n];
+          for (int n = 0; n < NW; ++n) wb[b][n] = own[b] ? ow[n] : bw[n];
         }
-        const bool run_own = b0 == 0 && other;
         for (int32_t f = base; f < cur; ++f) {
-          if (f > base && !(RB_FAN_EXP & 2)) {  // SaveGameState of frame f in every branch
+          if (f > base && !(RB_FAN_EXP & 2)) {  // SaveGameState of frame f in every chain
             const unsigned slot = static_cast<unsigned>(f % W);
 #pragma unroll
             for (int b = 0; b < NG; ++b)
-              if (on[b])
-                store_words<NW>(p.spec_cells + slot * NW * Gs, static_cast<int>(Gs),
-                                static_cast<int>(s * kSpecBranches + static_cast<unsigned>((b0 + b) * L + krot)), wb[b]);
-            if (run_own) store_words<NW>(p.spec_cells + slot * NW * Gs, static_cast<int>(Gs), static_cast<int>(ocol), ow);
+              if (on[b] || own[b])
+                store_words<NW>(p.spec_cells + slot * NW * Gs, static_cast<int>(Gs), static_cast<int>(col[b]), wb[b]);
           }
-#pragma unroll
-          for (int b = 0; b < NG; ++b) adv(wb[b], in[b], rs);
-          if (run_own) {
+          uint32_t v = 0;  // the other player's input of frame f
+          if (any_own) {
             const int j = f - base;
-            uint32_t v;
             if (j < kFanPre) v = fan_input(vpk, j);
             else if (own_local || (la_own != kNullFrame && f <= la_own)) v = ring.get(f, h_own, s);  // Confirmed
             else v = pred_own;  // repeat-last prediction (blank before the first input)
-            adv(ow, static_cast<InRec>(static_cast<uint64_t>(v) << (8 * h_own)), h_own);
           }
+          const InRec vo = static_cast<InRec>(static_cast<uint64_t>(v) << (8 * h_own));
+#pragma unroll
+          for (int b = 0; b < NG; ++b) adv(wb[b], own[b] ? vo : in[b], own[b] ? h_own : rs);
         }
-        if (run_own) store_words<NW>(p.spec_state, static_cast<int>(Gs), static_cast<int>(ocol), ow);
 #pragma unroll
         for (int b = 0; b < NG; ++b)
-          if (on[b])
-            store_words<NW>(p.spec_state, static_cast<int>(Gs),
-                            static_cast<int>(s * kSpecBranches + static_cast<unsigned>((b0 + b) * L + krot)), wb[b]);
+          if (on[b] || own[b]) store_words<NW>(p.spec_state, static_cast<int>(Gs), static_cast<int>(col[b]), wb[b]);
       };
-      // Only the chains some lane of the wave needs: branch slot b0 + b of lane krot is branch
-      // (b0 + b) * L + krot, needed when below the session's branch count (ex_game's 9 classes at
-      // P = 4: 3 chains per lane, not kFanGroup = 4; K = 8: 2).  Known at compile time for a
-      // whole-alphabet candidate set, a wave vote otherwise.
+      // the slots the wave runs: the most any of its lanes needs
+      constexpr int kMaxSlots = (kSpecBranches + P - 1 + static_cast<int>(L) - 1) / static_cast<int>(L);
+      int ns = 0;
 #pragma unroll
-      for (int b0 = 0; b0 < kB; b0 += kFanGroup) {
-        int ng = 0;
-        if constexpr (!kMtf) {
-          constexpr int n = AlphabetClasses<G>::value.n;
-          ng = min(kFanGroup, max(0, (n - b0 * static_cast<int>(L) + static_cast<int>(L) - 1) / static_cast<int>(L)));
-        } else {
+      for (int sb = 0; sb < kMaxSlots; ++sb) ns += __any(sb < nslots) ? 1 : 0;
 #pragma unroll
-          for (int b = 0; b < kFanGroup; ++b) ng += __any((b0 + b) * static_cast<int>(L) + krot < nb) ? 1 : 0;
-        }
-        if (ng == 0 && b0 > 0) break;  // (group 0 also runs the other players' chains)
-        if (ng <= 1) group(std::integral_constant<int, 1>{}, b0);
-        else if (ng == 2) group(std::integral_constant<int, 2>{}, b0);
-        else if (ng == 3) group(std::integral_constant<int, 3>{}, b0);
-        else group(std::integral_constant<int, 4>{}, b0);
+      for (int b0 = 0; b0 < kMaxSlots; b0 += kFanGroup) {
+        const int ng = min(kFanGroup, ns - b0);
+        if (ng <= 0) break;
+        const bool last = b0 + ng == ns;
+        if (ng == 1) group(std::integral_constant<int, 1>{}, b0, last);
+        else if (ng == 2) group(std::integral_constant<int, 2>{}, b0, last);
+        else if (ng == 3) group(std::integral_constant<int, 3>{}, b0, last);
+        else group(std::integral_constant<int, 4>{}, b0, last);
       }
       tot_branch += static_cast<uint32_t>(cur - base) * static_cast<uint32_t>(nb);
     }

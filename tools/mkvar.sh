@@ -8,7 +8,7 @@ cd "$(dirname "$0")/../ggrs_amd/csrc"
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -DRB_EXPERIMENTS=0 -mllvm -amdgpu-sched-strategy=max-ilp"
 name=$1; shift
 mkdir -p build/var ../var
-TUS="ops_exgame_p2"; [ -n "$ALLP" ] && TUS="ops_exgame_p1 ops_exgame_p2 ops_exgame_p3 ops_exgame_p4"
+TUS=${TUS:-ops_exgame_p2}; [ -n "$ALLP" ] && TUS="ops_exgame_p1 ops_exgame_p2 ops_exgame_p3 ops_exgame_p4"
 VOBJS=""
 for tu in $TUS; do
   /opt/rocm/bin/hipcc $F "$@" -c -o build/var/${tu}_$name.o $tu.hip &
