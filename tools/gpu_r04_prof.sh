@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 4 profile set (GPU box), in parts (one gpurun call each): every bench line's
-# rocprofv3 kernel stats + PMC passes (tools/prof_round.sh).  PART=1|2|3.
+# rocprofv3 kernel stats + PMC passes (tools/prof_round.sh).  PART=1|2|3|4.
 # Back here: tools/r04_fold.sh folds them into profiles/r04_*.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -10,7 +10,8 @@ case "${PART:-1}" in
 1)
   p driver "--ticks-per-launch 20" 20 20 &&
   p synctest "" 400 50 &&
-  p synctest1 "--ticks-per-launch 1" 100 50 &&
+  p synctest1 "--ticks-per-launch 1" 100 50 ;;
+4)
   p p2p "--session p2p" 400 50 &&
   p p2p1 "--session p2p --ticks-per-launch 1" 200 50 &&
   p p2p_sparse "--session p2p --sparse-saving" 400 50 ;;

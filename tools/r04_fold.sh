@@ -26,4 +26,4 @@ f brawler "$B" 50
 f brawler1 "$B tpl=1" 1
 f brawler_p2p "$QB" 50
 f brawler_p2p_sparse "$QB sparse" 50
-f brawler_fan "$QB fanout ${BRAWLER_FAN_TPL_KEY:-tpl=1}" 1
+f brawler_fan "$QB fanout tpl=20" 1  # (one call of 20 ticks: a P2P and a fan-out launch per tick)
