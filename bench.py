@@ -494,7 +494,8 @@ def bench_p2p(args):
                                   f"p2p_kernel<{gname}>" + ((" + fanout_kernel (per tick)" if generic_fan or brawler
                                                              else " with the in-kernel fan-out (fused P2P ticks)")
                                                             if args.fanout
-                                                            else " (fused P2P ticks)"),
+                                                            else (" (one tick per launch)" if tl == 1 else
+                                                                  " (fused P2P ticks)")),
                                   pmc_profile(cfg_key), "algorithmic: cells loaded/saved, inputs, deliveries")
         line = {
             "metric": "P2P session-frames simulated/sec (node), rollback to the first mispredicted frame",
