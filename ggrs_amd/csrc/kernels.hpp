@@ -32,6 +32,33 @@
 
 namespace rb {
 
+// ---- Issue-priority turns for the waves that share a SIMD (round 4, tools/wave_clock.py).
+// At 65,536 sessions the fused kernels run two waves per SIMD, and the SIMD's arbiter issues
+// the older wave first whenever both are ready: per-wave clocks showed the first wave of every
+// SIMD finishing a 50-tick SyncTest launch in ~130 us and the second in ~200 us, the second
+// running alone (one wave: a latency-bound chain) for the last third of the launch.  Taking
+// turns at the higher priority (s_setprio), switched on the chip's constant-rate clock every
+// 2^RB_PRIO_SHIFT x 10 ns and keyed to the wave's slot on its SIMD (HW_ID bit 0: the two waves
+// of a SIMD hold slots 0 and 1), lets both progress at the pair's rate and finish together.
+// Quanta measured (SyncTest, 50 ticks): 2^10 205, 2^11 201, 2^12 200 us against 217; checking
+// every AdvanceFrame instead of every tick: 212.
+#ifndef RB_PRIO_SHIFT
+#define RB_PRIO_SHIFT 11
+#endif
+#ifndef RB_STEADY_PRIO
+#define RB_STEADY_PRIO 1  // 0: the hardware's oldest-first order (A/B builds)
+#endif
+#ifndef RB_P2P_PRIO
+#define RB_P2P_PRIO 1
+#endif
+__device__ __forceinline__ uint32_t wave_slot_parity() { return __builtin_amdgcn_s_getreg(0xF804) & 1u; }  // HW_ID
+__device__ __forceinline__ void prio_turn(uint32_t wslot) {
+  if (((static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime() >> RB_PRIO_SHIFT) ^ wslot) & 1u) != 0u)
+    __builtin_amdgcn_s_setprio(1);
+  else
+    __builtin_amdgcn_s_setprio(0);
+}
+
 constexpr int kChunk = 8;  // inputs prefetched per chunk of AdvanceFrames
 constexpr int kMaxRepl = 8;
 
@@ -389,6 +416,15 @@ using DecOf = typename DecSel<G>::type;
 #ifndef RB_STEADY_WAVES_PER_EU
 #define RB_STEADY_WAVES_PER_EU 0  // >0: the occupancy the compiler may schedule for (A/B builds)
 #endif
+// RB_WAVE_CLOCK (A/B builds, tools/wave_clock.py): every wave of the steady kernel records its
+// start and end on the chip's constant-rate clock (s_memrealtime, 100 MHz) and where it ran
+// (HW_ID, XCC_ID) into rb_wave_clock, read back by rb_debug_wave_clock.
+#ifndef RB_WAVE_CLOCK
+#define RB_WAVE_CLOCK 0
+#endif
+#if RB_WAVE_CLOCK
+__device__ uint64_t rb_wave_clock[4 * 8192];
+#endif
 template <class G, int CD, bool kExp>
 __global__ void __launch_bounds__(256)
 #if RB_STEADY_WAVES_PER_EU > 0
@@ -414,6 +450,10 @@ steady_kernel(const RunParams p) {
   }
   const unsigned Spad = static_cast<unsigned>(p.Spad), Gpad = Spad * L;
   const unsigned slot_words = static_cast<unsigned>(NW) * Gpad;
+#if RB_WAVE_CLOCK
+  const uint64_t wc_start = __builtin_amdgcn_s_memrealtime();
+  uint32_t wc_general = 0;  // ticks this wave ran in the general (not in-range) form
+#endif
   InRec* __restrict__ ring = reinterpret_cast<InRec*>(p.ring);
   CS* __restrict__ csa = reinterpret_cast<CS*>(p.cs);
   CS* __restrict__ fsa = reinterpret_cast<CS*>(p.fs);
@@ -492,9 +532,15 @@ steady_kernel(const RunParams p) {
   for (int k = 0; k + 1 < CD; ++k) settle(fsw[k]);
   settle(newin);
   if constexpr (G::kDisplay) settle(pc);
+#if RB_STEADY_PRIO
+  const uint32_t wslot = wave_slot_parity();
+#endif
   for (int t = 0; t < p.T; ++t) {
     const int c = p.c0 + t;
     const bool more = t + 1 < p.T;
+#if RB_STEADY_PRIO
+    if (p.T > 1) prio_turn(wslot);  // (launch-uniform)
+#endif
     // ---- the next tick's inputs (read-only sources), before this tick's stores
     const InRec newin_next = new_input(more ? t + 1 : t);
     const InRec next_last = input_of_frame(more ? c + 1 : c);  // frame f0+CD+1 of the next tick
@@ -578,6 +624,9 @@ steady_kernel(const RunParams p) {
         steps(std::true_type{}, std::false_type{});
       }
     } else {
+#if RB_WAVE_CLOCK
+      ++wc_general;
+#endif
       steps(std::false_type{}, std::false_type{});
     }
     if constexpr (G::kDisplay) {
@@ -631,7 +680,23 @@ steady_kernel(const RunParams p) {
     f0 += 1;
     slot0 = slot_after(slot0, 1);
   }
+#if RB_WAVE_CLOCK
+  const uint64_t wc_end = __builtin_amdgcn_s_memrealtime();
+  const unsigned wv = g / 64;
+  if ((g & 63u) == 0 && wv < 8192) {
+    rb_wave_clock[4 * wv + 0] = wc_start;
+    rb_wave_clock[4 * wv + 1] = wc_end;
+    rb_wave_clock[4 * wv + 2] = static_cast<uint64_t>(__builtin_amdgcn_s_getreg(0xF814)) << 32 |  // XCC_ID
+                                __builtin_amdgcn_s_getreg(0xF804);                               // HW_ID
+    rb_wave_clock[4 * wv + 3] = wc_general;
+  }
+#endif
 }
+#if RB_WAVE_CLOCK
+extern "C" int rb_debug_wave_clock(uint64_t* host_out, int n) {
+  return static_cast<int>(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(rb_wave_clock), sizeof(uint64_t) * 4 * min(n, 8192)));
+}
+#endif
 
 }  // namespace rb
 #if RB_EXPERIMENTS

@@ -1771,9 +1771,16 @@ p2p_kernel(const P2PParams p) {
     tick_rotate();
     return true;
   };
+#if RB_P2P_PRIO
+  const uint32_t wslot = wave_slot_parity();  // (kernels.hpp prio_turn)
+#endif
   if constexpr (!kAsync) {
-    for (int t = 0; t < p.T; ++t)
+    for (int t = 0; t < p.T; ++t) {
+#if RB_P2P_PRIO
+      if (p.T > 1) prio_turn(wslot);
+#endif
       if (!tick(t)) break;
+    }
   } else {
     // lane-asynchronous ticks (see kAsync above): one AdvanceFrame per session per iteration
     int t = 0, count = 0, i = 0;
@@ -1782,6 +1789,9 @@ p2p_kernel(const P2PParams p) {
     [[maybe_unused]] bool checked = false;  // kSparse: check_last_saved_state already ran this tick
     [[maybe_unused]] uint32_t iters = 0;
     while (inres || (!stopped && t < p.T)) {
+#if RB_P2P_PRIO
+      prio_turn(wslot);
+#endif
       if constexpr (RB_P2P_EXP & 4) ++iters;
       if (!inres) {  // the next tick's opening, up to its rollback's LoadGameState
         const int r = tick_begin(t);
