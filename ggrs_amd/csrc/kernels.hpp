@@ -41,7 +41,8 @@ namespace rb {
 // 2^RB_PRIO_SHIFT x 10 ns and keyed to the wave's slot on its SIMD (HW_ID bit 0: the two waves
 // of a SIMD hold slots 0 and 1), lets both progress at the pair's rate and finish together.
 // Quanta measured (SyncTest, 50 ticks): 2^10 205, 2^11 201, 2^12 200 us against 217; checking
-// every AdvanceFrame instead of every tick: 212.
+// every AdvanceFrame instead of every tick: 212.  One-tick launches (T = 1) take no turns:
+// 2^7-2^9 quanta checked at the tick's opening and every AdvanceFrame measured no gain.
 #ifndef RB_PRIO_SHIFT
 #define RB_PRIO_SHIFT 11
 #endif

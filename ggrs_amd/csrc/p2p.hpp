@@ -1406,6 +1406,7 @@ p2p_kernel(const P2PParams p) {
   constexpr bool kPrefetch = !kSpec || kInFan;
   auto tick_begin = [&](int t) __attribute__((always_inline)) -> int {
     const int tn = t + 1 < p.T ? t + 1 : t;
+
     if constexpr (kPrefetch) {
 #pragma unroll
       for (int j = 0; j < PPL; ++j) {
