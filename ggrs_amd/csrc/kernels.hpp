@@ -41,7 +41,10 @@ namespace rb {
 // 2^RB_PRIO_SHIFT x 10 ns and keyed to the wave's slot on its SIMD (HW_ID bit 0: the two waves
 // of a SIMD hold slots 0 and 1), lets both progress at the pair's rate and finish together.
 // Quanta measured (SyncTest, 50 ticks): 2^10 205, 2^11 201, 2^12 200 us against 217; checking
-// every AdvanceFrame instead of every tick: 212.  One-tick launches (T = 1) take no turns:
+// every AdvanceFrame instead of every tick: 212.  Turns by progress instead of the clock (512-thread
+// workgroups, the two waves of a SIMD posting their tick counts in LDS) equalised every pair but
+// not the launch: what is left is the spread between SIMDs, whose waves take the speed clamp
+// (ex_game.rs:300-304) in different numbers of frames (lifetime correlation 0.66).  One-tick launches (T = 1) take no turns:
 // 2^7-2^9 quanta checked at the tick's opening and every AdvanceFrame measured no gain.
 #ifndef RB_PRIO_SHIFT
 #define RB_PRIO_SHIFT 11
@@ -454,6 +457,7 @@ steady_kernel(const RunParams p) {
 #if RB_WAVE_CLOCK
   const uint64_t wc_start = __builtin_amdgcn_s_memrealtime();
   uint32_t wc_general = 0;  // ticks this wave ran in the general (not in-range) form
+  uint32_t wc_clamp = 0;
 #endif
   InRec* __restrict__ ring = reinterpret_cast<InRec*>(p.ring);
   CS* __restrict__ csa = reinterpret_cast<CS*>(p.cs);
@@ -596,8 +600,15 @@ steady_kernel(const RunParams p) {
         w[0] += win[k];
       else if constexpr (kFast && !kExp)
         advance_fast<G>(w, prep, k, special);  // AdvanceFrame{inputs}
-      else if constexpr (G::kHasPrep && !kExp)
+      else if constexpr (G::kHasPrep && !kExp) {
+#if RB_WAVE_CLOCK
+        {  // (wave clocks: frames in which some lane of the wave takes the speed clamp)
+          const float vx = __uint_as_float(w[2]) * G::kFriction + prep.tx[0][k], vy = __uint_as_float(w[3]) * G::kFriction + prep.ty[0][k];
+          wc_clamp += __any(vx * vx + vy * vy > 49.0f) ? 1u : 0u;
+        }
+#endif
         G::advance_prepared(w, prep, k);  // AdvanceFrame{inputs}
+      }
       else
         G::template advance<kInRange>(w, (dbg & 32u) ? static_cast<InRec>(win[k] & static_cast<InRec>(dbg >> 8)) : win[k],
                                       lane, 0u, &p.counters[1]);  // AdvanceFrame{inputs}
@@ -689,7 +700,7 @@ steady_kernel(const RunParams p) {
     rb_wave_clock[4 * wv + 1] = wc_end;
     rb_wave_clock[4 * wv + 2] = static_cast<uint64_t>(__builtin_amdgcn_s_getreg(0xF814)) << 32 |  // XCC_ID
                                 __builtin_amdgcn_s_getreg(0xF804);                               // HW_ID
-    rb_wave_clock[4 * wv + 3] = wc_general;
+    rb_wave_clock[4 * wv + 3] = wc_general | (blockDim.x / 64u) << 16 | static_cast<uint64_t>(wc_clamp) << 40;
   }
 #endif
 }

@@ -30,9 +30,13 @@ for c in range(W0, T, TPL):
     assert lib.rb_debug_wave_clock(buf.ctypes.data_as(ctypes.c_void_p), 8192) == 0
     nw = (S * 2 + 63) // 64
     r = buf.reshape(-1, 4)[:nw].astype(np.int64)
-    st, en, hw, gen = r[:, 0], r[:, 1], r[:, 2], r[:, 3]
+    st, en, hw, gen = r[:, 0], r[:, 1], r[:, 2], r[:, 3] & 0xFF
     t0 = st.min()
     life = (en - st) / 100.0  # us
+    extra = r[:, 3]
+    clamp = extra >> 40
+    print(f"  block waves {np.unique((extra >> 16) & 0xFF)}; frames with a clamp per wave mean {clamp.mean():.0f} of "
+          f"{8 * TPL}, min/max {clamp.min()}/{clamp.max()}; lifetime corr {np.corrcoef(clamp, life)[0, 1]:.2f}")
     span = (en.max() - t0) / 100.0
     xcc = (hw >> 32) & 0xF
     hid = hw & 0xFFFFFFFF
@@ -45,7 +49,10 @@ for c in range(W0, T, TPL):
     print(f"  general-form ticks per wave: mean {gen.mean():.2f}, max {gen.max()}; lifetime corr {np.corrcoef(gen, life)[0, 1]:.2f}"
           if gen.std() > 0 else "  no general-form ticks")
     slot = hid & 0xF
-    blk = np.arange(nw) // 4
+    BS = int(os.environ.get("BLOCK_WAVES", 4))
+    blk = np.arange(nw) // BS
+    wib = np.arange(nw) % BS
+    print(f"  waves on SIMD (wave in block % 4): {(simd == wib % 4).mean():.2f} of waves")
     print("  lifetime by HW wave slot: " + " ".join(f"{w}:{life[slot == w].mean():.1f}(n={int((slot == w).sum())})"
                                                      for w in range(16) if (slot == w).any()))
     print("  lifetime by block index < or >= 256: %.1f / %.1f" % (life[blk < 256].mean(), life[blk >= 256].mean()))
