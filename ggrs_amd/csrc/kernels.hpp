@@ -55,12 +55,32 @@ namespace rb {
 #ifndef RB_P2P_PRIO
 #define RB_P2P_PRIO 1
 #endif
-__device__ __forceinline__ uint32_t wave_slot_parity() { return __builtin_amdgcn_s_getreg(0xF804) & 1u; }  // HW_ID
-__device__ __forceinline__ void prio_turn(uint32_t wslot) {
-  if (((static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime() >> RB_PRIO_SHIFT) ^ wslot) & 1u) != 0u)
+#ifndef RB_PRIO_ROTATE
+#define RB_PRIO_ROTATE 1  // 0: two-level turns whatever the waves per SIMD (A/B builds)
+#endif
+// The turn key: the wave's slot on its SIMD (HW_ID bits 1:0) and, in bit 2, whether the launch
+// puts more than two waves on a SIMD (1,024 SIMDs on MI355X).  Two waves take turns at priority
+// 1 over 0; three or four rotate through priorities 0-3 (each leads a quarter of the time).
+// Measured at 131,072 sessions (4 waves per SIMD): SyncTest 8.58 us per tick rotating, 8.78 with
+// two-level turns, 8.85 without turns; P2P 7.01 / 6.76 / 7.22, so p2p_kernel keeps two levels.
+__device__ __forceinline__ uint32_t wave_turn_key() {
+  const bool many = RB_PRIO_ROTATE && gridDim.x * blockDim.x > 2u * 64u * 1024u;
+  return (__builtin_amdgcn_s_getreg(0xF804) & 3u) | (many ? 4u : 0u);  // HW_ID
+}
+__device__ __forceinline__ void prio_turn(uint32_t key) {
+  const uint32_t c = static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime() >> RB_PRIO_SHIFT);
+  if (key & 4u) {
+    switch ((c + key) & 3u) {
+      case 0: __builtin_amdgcn_s_setprio(0); break;
+      case 1: __builtin_amdgcn_s_setprio(1); break;
+      case 2: __builtin_amdgcn_s_setprio(2); break;
+      default: __builtin_amdgcn_s_setprio(3); break;
+    }
+  } else if (((c ^ key) & 1u) != 0u) {
     __builtin_amdgcn_s_setprio(1);
-  else
+  } else {
     __builtin_amdgcn_s_setprio(0);
+  }
 }
 
 constexpr int kChunk = 8;  // inputs prefetched per chunk of AdvanceFrames
@@ -538,7 +558,7 @@ steady_kernel(const RunParams p) {
   settle(newin);
   if constexpr (G::kDisplay) settle(pc);
 #if RB_STEADY_PRIO
-  const uint32_t wslot = wave_slot_parity();
+  const uint32_t wslot = wave_turn_key();
 #endif
   for (int t = 0; t < p.T; ++t) {
     const int c = p.c0 + t;

@@ -1773,7 +1773,8 @@ p2p_kernel(const P2PParams p) {
     return true;
   };
 #if RB_P2P_PRIO
-  const uint32_t wslot = wave_slot_parity();  // (kernels.hpp prio_turn)
+  const uint32_t wslot = wave_turn_key() & 3u;  // (kernels.hpp prio_turn: two-level turns, measured
+                                                // better than the rotation at 4 waves per SIMD here)
 #endif
   if constexpr (!kAsync) {
     for (int t = 0; t < p.T; ++t) {
