@@ -732,6 +732,29 @@ constexpr int kFanGroup = 4;  // branches a lane advances together (its independ
 // kMtf (fan-out batches only): the candidates come from the queues' move-to-front lists, for an
 // alphabet larger than K; otherwise (ex_game at K = 16) they are the alphabet itself, and the lists
 // are neither kept nor read (no registers held for them).
+// RB_P2P_PHASE (A/B builds, tools/p2p_phase.py): one-tick launches record, per wave, the
+// constant-rate clock (100 MHz) at entry, once the state loads are in, after the poll and
+// threshold decision, after the rollback and saves, after the tick's own frame, and at the end.
+// Measured at 65,536 sessions (p50 / p90 us): state loads 1.28 / 1.52, poll + threshold 1.44 /
+// 1.60, rollback + saves 2.40 / 3.16, the tick's frame 0.84 / 1.00, epilogue 0.76 / 0.92; first
+// entry to last end 8.6 of the launch's 10.4.  Fetching the likely rollback cell with the first
+// deliveries (one round trip fewer) cut the rollback phase to 2.16 but not the launch (A/B,
+// dropped); so did the LDS input ring (11.7-12.5 against 10.4-11.0 us one-tick, but 5.0 against
+// 5.6 us per tick in 8-tick launches).
+#ifndef RB_P2P_PHASE
+#define RB_P2P_PHASE 0
+#endif
+#if RB_P2P_PHASE
+__device__ uint64_t rb_p2p_phase[8 * 4096];
+#define RB_PH(i)                                                    \
+  do {                                                              \
+    if (p.T == 1) ph[i] = __builtin_amdgcn_s_memrealtime();         \
+  } while (0)
+#else
+#define RB_PH(i) \
+  do {           \
+  } while (0)
+#endif
 template <class G, bool kSpec, bool kSparse, bool kNet, bool kLdsC, bool kAsync, bool kWire = false, bool kMtf = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RB_P2P_WAVES_PER_EU)))
 p2p_kernel(const P2PParams p) {
@@ -749,6 +772,10 @@ p2p_kernel(const P2PParams p) {
   const int lane = static_cast<int>(g % L);
   const bool lead = lane == 0;
   if (s >= static_cast<unsigned>(p.S)) return;  // whole lane groups leave together
+#if RB_P2P_PHASE
+  uint64_t ph[6] = {0, 0, 0, 0, 0, 0};
+#endif
+  RB_PH(0);
   // A session that hit a reference assert stays stopped (the reference
   // process would have aborted): it reports RB_PANIC from then on and its
   // state, cells and queues stay as the panic left them.  (Checked once the
@@ -894,29 +921,20 @@ p2p_kernel(const P2PParams p) {
     return r;
   };
   if (panicked) return;
+#if RB_P2P_PHASE
+  settle(static_cast<uint32_t>(cur));
+  settle(w[0]);
+  settle(static_cast<uint32_t>(q[0].last_req));
+  settle(static_cast<uint32_t>(up[0]));
+#endif
+  RB_PH(1);
   // LDS queue: the HBM frames this launch can read.  Reads are of frames
   // >= cur - W (adjust_gamestate checks that before it advances) up to the
   // last added one, or of the last added frame itself (predictions and the
   // delay replication); every later frame is added inside the launch.  (The
   // fan-out's candidates come from the queue's move-to-front list, not from
   // these frames: fan_candidates.)
-  const int32_t la0 = q[0].last_added;
-  if constexpr (kLdsQ) {
-    const int h = player_of(0);
-    // (and a packet's reference input, frame start - 1 >= last received - 2 * max_prediction)
-    const int32_t back = kWire ? 2 * W + 1 : 0;
-    if (h < P && la0 != kNullFrame) {
-      const int32_t lo = max(max(0, la0 - (kQueueLen - 1)), min(cur - W, la0) - back);
-      for (int32_t f0 = lo; f0 <= la0; f0 += 8) {  // 8 loads in flight per round trip
-        uint32_t v[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = hbm.get(min(f0 + k, la0), h, s);
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if (f0 + k <= la0) ring.put(f0 + k, h, s, v[k]);
-      }
-    }
-  }
+  const int32_t la0 = q[0].last_added;  // (the LDS queue's fill: after the first deliveries' loads, below)
 
   if constexpr (kLdsC) {  // the snapshot ring of this launch's sessions into LDS
 #pragma unroll
@@ -1244,6 +1262,28 @@ p2p_kernel(const P2PParams p) {
     const int32_t f = remote_start(j);
 #pragma unroll
     for (int k = 0; k < kPre; ++k) rv[j][k] = load_remote(j, f + k);
+  }
+  // LDS queue: the HBM frames this launch can read, loaded in the same round trip as the first
+  // deliveries above.  Reads are of frames >= cur - W (adjust_gamestate checks that before it
+  // advances) up to the last added one, or of the last added frame itself (predictions and the
+  // delay replication); every later frame is added inside the launch.  (The fan-out's candidates
+  // come from the queue's move-to-front list, not from these frames: fan_candidates.)
+  if constexpr (kLdsQ) {
+    const int h = player_of(0);
+    // (and a packet's reference input, frame start - 1 >= last received - 2 * max_prediction)
+    const int32_t back = kWire ? 2 * W + 1 : 0;
+    if (h < P && la0 != kNullFrame) {
+      const int32_t lo = max(max(0, la0 - (kQueueLen - 1)), min(cur - W, la0) - back);
+      constexpr int kFill = 16;  // loads in flight per round trip
+      for (int32_t f0 = lo; f0 <= la0; f0 += kFill) {
+        uint32_t v[kFill];
+#pragma unroll
+        for (int k = 0; k < kFill; ++k) v[k] = hbm.get(min(f0 + k, la0), h, s);
+#pragma unroll
+        for (int k = 0; k < kFill; ++k)
+          if (f0 + k <= la0) ring.put(f0 + k, h, s, v[k]);
+      }
+    }
   }
 
 
@@ -1756,9 +1796,11 @@ p2p_kernel(const P2PParams p) {
   };
   auto tick = [&](int t) __attribute__((always_inline)) -> bool {
     const int r = tick_begin(t);
+    RB_PH(2);
     if (r == 0) return false;
     if (r == 2) {
       rollback_and_save();
+      RB_PH(3);
       if (status == kP2PStatusPanic) return false;
       if (!run_desync()) {
         status = kP2PStatusPanic;
@@ -1767,6 +1809,10 @@ p2p_kernel(const P2PParams p) {
       add_local();
       advance(cur);
       next_frame();
+#if RB_P2P_PHASE
+      settle(w[0]);
+#endif
+      RB_PH(4);
     }
     if (in_fan) fan_inlane();
     tick_rotate();
@@ -1947,7 +1993,21 @@ p2p_kernel(const P2PParams p) {
       }
     }
   }
+#if RB_P2P_PHASE
+  RB_PH(5);
+  if (p.T == 1 && (g & 63u) == 0 && g / 64 < 4096) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) rb_p2p_phase[8 * (g / 64) + i] = ph[i];
+    rb_p2p_phase[8 * (g / 64) + 6] = static_cast<uint64_t>(__builtin_amdgcn_s_getreg(0xF814)) << 32 | __builtin_amdgcn_s_getreg(0xF804);
+    rb_p2p_phase[8 * (g / 64) + 7] = static_cast<uint64_t>(tot_load) << 32 | tot_adv;
+  }
+#endif
 }
+#if RB_P2P_PHASE
+extern "C" int rb_debug_p2p_phase(uint64_t* host_out, int n) {
+  return static_cast<int>(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(rb_p2p_phase), sizeof(uint64_t) * 8 * min(n, 4096)));
+}
+#endif
 
 // ---------------------------------------------------------------------------
 // Speculative branch fan-out (BASELINE config 4).  After a
