@@ -885,6 +885,16 @@ struct GameOpsT final : GameOps {
         return rb_launch(k, dim3(grid), dim3(block), static_cast<uint32_t>(lds), st, ev, p);
       }
     }
+    if constexpr (!kSpec && !kNet && p2p_lds_queue<G>() && G::kLanes > 1) {
+      if (p.T >= kLdsQMinTicks) {  // the input ring alone in LDS (kLdsQMinTicks)
+        auto k = p2p_kernel<G, kSpec, kSparse, kNet, false, false, false, kMtf, true>;
+        lds = p2p_lds_bytes<G, true>(block);
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           static_cast<int>(lds));
+        if (e != hipSuccess) return e;
+        return rb_launch(k, dim3(grid), dim3(block), static_cast<uint32_t>(lds), st, ev, p);
+      }
+    }
     return rb_launch(p2p_kernel<G, kSpec, kSparse, kNet, false, false, false, kMtf>, dim3(grid), dim3(block),
                      static_cast<uint32_t>(lds), st, ev, p);
   }

@@ -599,6 +599,14 @@ constexpr size_t kLdsPerBlockMax = 80 * 1024;
 // ring in and out costs more than it saves below about 24 ticks (measured: HBM
 // cells 4.8 us per tick at 16 ticks per launch, LDS cells 4.1 at 32)
 constexpr int kLdsCellsMinTicks = RB_LDS_CELLS_MIN_TICKS;
+// Launches of kLdsQMinTicks up to kLdsCellsMinTicks ticks keep the cells in HBM but the input ring
+// in LDS (p2p_kernel kQ; plain path and sparse saving, ex_game's lane-per-player layout).  Measured
+// at 65,536 sessions, us per tick (HBM ring / LDS ring / LDS cells): 2 ticks per launch 7.6 / 8.0 /
+// 12.7, 4: 6.34 / 6.08 / 8.44, 8: 5.57 / 5.02 / 5.97, 16: 5.07 / 4.36 / 4.55 (tools/ab_short.sh).
+#ifndef RB_LDSQ_MIN_TICKS
+#define RB_LDSQ_MIN_TICKS 4
+#endif
+constexpr int kLdsQMinTicks = RB_LDSQ_MIN_TICKS;
 template <class G>
 constexpr bool p2p_lds_cells(int W, int block) {
   return p2p_lds_queue<G>() && W <= kLdsCellsMaxW &&
@@ -755,7 +763,8 @@ __device__ uint64_t rb_p2p_phase[8 * 4096];
   do {           \
   } while (0)
 #endif
-template <class G, bool kSpec, bool kSparse, bool kNet, bool kLdsC, bool kAsync, bool kWire = false, bool kMtf = false>
+template <class G, bool kSpec, bool kSparse, bool kNet, bool kLdsC, bool kAsync, bool kWire = false, bool kMtf = false,
+          bool kQ = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RB_P2P_WAVES_PER_EU)))
 p2p_kernel(const P2PParams p) {
   static_assert(!kAsync || (kLdsC && !kSpec && !kNet), "lane-asynchronous ticks: plain or sparse path, LDS cells");
@@ -786,7 +795,7 @@ p2p_kernel(const P2PParams p) {
   const unsigned slot_words = static_cast<unsigned>(NW) * Gpad;
   const int W = p.W;
   CS* __restrict__ csa = reinterpret_cast<CS*>(p.cs);
-  constexpr bool kLdsQ = p2p_lds_queue_in<G, kLdsC>();
+  constexpr bool kLdsQ = p2p_lds_queue_in<G, kLdsC || kQ>();  // (kQ: the input ring alone, see kLdsQMinTicks)
   const RingIO<IB> hbm{reinterpret_cast<uint8_t*>(p.ring), P, p.Spad};
   extern __shared__ uint8_t lds_queue[];
   const auto ring = [&]() __attribute__((always_inline)) {

@@ -117,7 +117,7 @@ def test_gpu_p2p_bench_path_at_full_size(gpu_available, sparse):
 def test_gpu_p2p_one_tick_launches_at_full_size(gpu_available):
     """Live play (one launch per tick, the cells and the input ring in HBM) at 65,536 sessions
     equals the fused 50-tick launches (LDS rings, lane-asynchronous ticks) bit for bit, and the
-    oracle sample."""
+    oracle sample; so do 8-tick launches (HBM cells, the input ring in LDS)."""
     P, T = 2, 60
     (inputs, upto, rin), (di, du, dr) = network(P, T)
     live, fused = batch(P), batch(P)
@@ -130,6 +130,10 @@ def test_gpu_p2p_one_tick_launches_at_full_size(gpu_available):
     fused.run_ticks(di[30:], du[30:], dr)
     assert_same_batch(live, fused, "one-tick vs fused launches")
     assert live.counters()[2] == 0 and live.totals()[:3] == fused.totals()[:3]
+    mid = batch(P)  # 8-tick launches: HBM cells, the input ring in LDS (p2p.hpp kLdsQMinTicks)
+    for t0 in range(0, T, 8):
+        mid.run_ticks(di[t0:t0 + 8], du[t0:t0 + 8], dr)
+    assert_same_batch(mid, fused, "8-tick vs fused launches")
 
 
 def test_gpu_c4_fanout_at_full_size(gpu_available):
