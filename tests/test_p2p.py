@@ -321,6 +321,7 @@ FUSED_CASES = [  # game, P, W, d, rd, local_mask, lag range, ticks per launch, s
     # launches of 4-23 ticks: HBM cells, the input ring in LDS (p2p.hpp kLdsQMinTicks)
     (G.Game.EX_GAME, 2, 8, 2, 1, 0b10, (1, 5), 8, True),
     (G.Game.EX_GAME, 3, 7, 0, 2, 0b010, (0, 4), 5, False),
+    (G.Game.BRAWLER, 2, 8, 2, 2, 0b01, (1, 4), 10, False),  # the brawler: HBM cells, LDS input ring
 ]
 
 
