@@ -929,6 +929,13 @@ p2p_kernel(const P2PParams p) {
     r.w0[0] = a.x, r.w0[1] = a.y, r.w0[2] = a.z, r.w0[3] = a.w, r.w0[4] = b.x, r.w0[5] = b.y, r.w0[6] = b.z, r.w0[7] = b.w;
     return r;
   };
+  // kWire: the first tick's packet heads, with the state loads (their addresses depend on nothing
+  // loaded), so the poll's decode waits one round trip less
+  [[maybe_unused]] PkHead pre0[PPL];
+  if constexpr (kWire) {
+#pragma unroll
+    for (int j = 0; j < PPL; ++j) pre0[j] = wire_fetch(min(player_of(j), P - 1), 0);
+  }
   if (panicked) return;
 #if RB_P2P_PHASE
   settle(static_cast<uint32_t>(cur));
@@ -1311,7 +1318,7 @@ p2p_kernel(const P2PParams p) {
       return kWireNothing;
     } else {
       const size_t idx = (static_cast<size_t>(t) * P + static_cast<size_t>(h)) * static_cast<size_t>(p.S) + s;
-      const PkHead hd = wire_fetch(h, t);
+      const PkHead hd = t == 0 ? pre0[j] : wire_fetch(h, t);
       const int32_t n = hd.n, start = hd.start;
       const uint8_t* pk = p.packets + static_cast<int64_t>(idx) * p.packet_stride;
       uint32_t w0[8];
