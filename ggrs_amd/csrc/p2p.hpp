@@ -805,6 +805,10 @@ p2p_kernel(const P2PParams p) {
   // the in-kernel fan-out (the batch's branches are this kernel's own unless fan_generic)
   constexpr bool kInFan = kSpec && inlane_fan<G>();
   const bool in_fan = kInFan && !p.fan_generic;
+  // The next tick's deliveries are prefetched, except by the P2P launches of
+  // the two-launch fan-out (fanout_kernel), which are always of one tick (the
+  // fan-out runs between ticks): there they would only hold registers.
+  constexpr bool kPrefetch = !kSpec || kInFan;
   static_assert(!kLdsC || (kLdsQ && (!kSpec || kInFan) && !kNet),
                 "the LDS snapshot ring needs the LDS queue; fanout_kernel and desync detection read HBM cells mid-launch");
   const unsigned bd = blockDim.x, tid = threadIdx.x, sl = tid / L, bps = bd / L;
@@ -930,7 +934,8 @@ p2p_kernel(const P2PParams p) {
     return r;
   };
   // kWire: the first tick's packet heads, with the state loads (their addresses depend on nothing
-  // loaded), so the poll's decode waits one round trip less
+  // loaded), so the poll's decode waits one round trip less; each later tick's come one tick
+  // ahead (pre_n, with the other deliveries)
   [[maybe_unused]] PkHead pre0[PPL];
   if constexpr (kWire) {
 #pragma unroll
@@ -1318,7 +1323,7 @@ p2p_kernel(const P2PParams p) {
       return kWireNothing;
     } else {
       const size_t idx = (static_cast<size_t>(t) * P + static_cast<size_t>(h)) * static_cast<size_t>(p.S) + s;
-      const PkHead hd = t == 0 ? pre0[j] : wire_fetch(h, t);
+      const PkHead hd = kPrefetch ? pre0[j] : (t == 0 ? pre0[j] : wire_fetch(h, t));  // (tick t's heads)
       const int32_t n = hd.n, start = hd.start;
       const uint8_t* pk = p.packets + static_cast<int64_t>(idx) * p.packet_stride;
       uint32_t w0[8];
@@ -1451,15 +1456,13 @@ p2p_kernel(const P2PParams p) {
   // returns); false when the session stops on a reference panic.
   int32_t up_n[PPL];
   uint32_t lin_n[PPL], rv_n[PPL][kPre];
+  [[maybe_unused]] PkHead pre_n[PPL];  // kWire: the next tick's packet heads
   [[maybe_unused]] int32_t pk_ds = kWireNothing;  // kWire: the last tick's decode status of this lane's endpoint
   uint32_t n_thr = 0;                             // PredictionThreshold ticks of this session in the launch
   // The tick's opening, through the PredictionThreshold decision: 0 = the
   // session stopped on a panic, 1 = the tick is over (Err(PredictionThreshold)),
   // 2 = rollback_and_save, add_local_input and the new frame follow.
-  // The next tick's deliveries are prefetched, except by the P2P launches of
-  // the two-launch fan-out (fanout_kernel), which are always of one tick (the
-  // fan-out runs between ticks): there they would only hold registers.
-  constexpr bool kPrefetch = !kSpec || kInFan;
+  // (the next tick's deliveries are prefetched unless kPrefetch is false, above)
   auto tick_begin = [&](int t) __attribute__((always_inline)) -> int {
     const int tn = t + 1 < p.T ? t + 1 : t;
 
@@ -1468,6 +1471,7 @@ p2p_kernel(const P2PParams p) {
       for (int j = 0; j < PPL; ++j) {
         up_n[j] = load_upto(tn, j);
         lin_n[j] = load_local(tn, j);
+        if constexpr (kWire) pre_n[j] = wire_fetch(min(player_of(j), P - 1), tn);
       }
     }
     status = kP2PStatusOk;
@@ -1807,6 +1811,7 @@ p2p_kernel(const P2PParams p) {
         lin[j] = lin_n[j];
 #pragma unroll
         for (int k = 0; k < kPre; ++k) rv[j][k] = rv_n[j][k];
+        if constexpr (kWire) pre0[j] = pre_n[j];
       }
     }
   };
