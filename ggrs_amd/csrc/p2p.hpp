@@ -699,7 +699,10 @@ constexpr bool inlane_fan() {
   if constexpr (IndepPlayers<G>::value) return G::kLanes > 1 && G::kLanes <= 4 && !G::kUsesStatus && G::kInputBytes == 1;
   else return false;
 }
-constexpr int kFanGroup = 4;  // branches a lane advances together (its independent chains)
+#ifndef RB_FAN_GROUP
+#define RB_FAN_GROUP 4  // A/B (tools/ab_fangroup.sh): 3 measured the same at C4 (206 VGPRs, still 2 waves per
+#endif                  // SIMD); 3 with a 3-waves cap (168 VGPRs, 160 B spilled) 8% slower
+constexpr int kFanGroup = RB_FAN_GROUP;  // chains a lane advances together (independent: instruction-level parallelism)
 #ifndef RB_FAN_INRANGE
 #define RB_FAN_INRANGE 1  // 0: the fan-out's chains always take the general AdvanceFrame (A/B builds)
 #endif
@@ -1796,9 +1799,9 @@ p2p_kernel(const P2PParams p) {
         if (ng <= 0) break;
         const bool last = b0 + ng == ns;
         if (ng == 1) group(std::integral_constant<int, 1>{}, b0, last);
-        else if (ng == 2) group(std::integral_constant<int, 2>{}, b0, last);
-        else if (ng == 3) group(std::integral_constant<int, 3>{}, b0, last);
-        else group(std::integral_constant<int, 4>{}, b0, last);
+        else if (ng == 2 || kFanGroup == 2) group(std::integral_constant<int, 2>{}, b0, last);
+        else if (ng == 3 || kFanGroup == 3) group(std::integral_constant<int, 3>{}, b0, last);
+        else group(std::integral_constant<int, (kFanGroup >= 4 ? 4 : 3)>{}, b0, last);
       }
       tot_branch += static_cast<uint32_t>(cur - base) * static_cast<uint32_t>(nb);
     }
