@@ -710,7 +710,8 @@ def main():
                 e1.record()
                 gather_ev.append((e0, e1))
                 desyncs.add_(shard.count_desynced(gathered, world, S, A))  # mismatch_frame != NULL_FRAME
-                audit_bad.add_(shard.audit_compare(gathered, world, S, A)[0])  # checksum of owner != replica
+                audit_bad.add_(shard.audit_compare(gathered, world, S, A, detail=False)[0])  # owner != replica
+                # (the count only: the detail list's nonzero() would stall the host inside the timed loop)
                 gathers[0] += 1
         return steady_launches
 

@@ -160,6 +160,7 @@ def test_audit_compare_finds_exactly_the_corrupted_replica():
     g2 = g.clone()
     g2[2 * (owned + audit) + owned + 1, 1] ^= 1  # high checksum word
     n, detail = shard.audit_compare(g2, world, owned, audit)
+    assert int(shard.audit_compare(g2, world, owned, audit, detail=False)[0]) == int(n)  # the bench's count-only form
     assert int(n) == 1
     assert detail.tolist() == [[1, 41, int(g[1, 0]), int(g[1, 0])]]
     # owned-row helpers skip the replicas
