@@ -641,6 +641,15 @@ def main():
     # and the warmup has run the fused steady kernel at least once.
     warm = cd + 1 + args.warmup
     RT = args.realtime_ticks  # one-tick-per-call ticks after the timed region (the 60 Hz serving path)
+    # Kernel timing.  An event pair on a launch (hipExtLaunchKernel) costs the host ~7 us per call
+    # and the timed wall ~12 us (tools/sync_probe.py, round 5), so by default the timed region
+    # launches without events ("twin"): a second batch, built and fed identically, runs the very same
+    # ticks with each launch timed by its own events right after the timed region; its sessions'
+    # states are bit-identical, so its launches do the same work.  GGRS_BENCH_EVENTS=launch times
+    # the timed region's own launches instead (rounds 3-4).
+    timing = os.environ.get("GGRS_BENCH_EVENTS", "twin")
+    if timing not in ("twin", "launch"):
+        raise SystemExit("GGRS_BENCH_EVENTS: twin or launch")
     T = warm + args.steps + RT
     # This rank's shard: global sessions [rank*S, (rank+1)*S); inputs keyed by global id.  With
     # N > 1 the batch also holds A audit replicas: the first A sessions of rank (r+1) % N.
@@ -656,17 +665,23 @@ def main():
 
     stream = torch.cuda.Stream(device=dev)
     game = G.Game.BRAWLER if brawler else G.Game.EX_GAME
-    sess = (G.SessionBuilder(game, num_sessions=S + A, device=local).with_num_players(P)
-            .with_max_prediction_window(args.max_prediction).with_check_distance(cd)
-            .with_input_delay(args.input_delay).with_checked_mismatches(False)
-            .with_block_size(args.block_size).start_synctest_session())
-    sess.set_stream(stream)
+
+    def new_batch():
+        b = (G.SessionBuilder(game, num_sessions=S + A, device=local).with_num_players(P)
+             .with_max_prediction_window(args.max_prediction).with_check_distance(cd)
+             .with_input_delay(args.input_delay).with_checked_mismatches(False)
+             .with_block_size(args.block_size).start_synctest_session())
+        b.set_stream(stream)
+        return b
+
+    sess = new_batch()
+    twin = new_batch() if timing == "twin" else None  # (the brawler's 4 GiB ring twice: 8 GiB of 288)
     reports = torch.zeros((S + A, shard.REPORT_WORDS), dtype=torch.int64, device=dev)  # rb_checksum_report, 24 B
     desyncs = torch.zeros((), dtype=torch.int64, device=dev)  # sessions reporting MismatchedChecksum
     audit_bad = torch.zeros((), dtype=torch.int64, device=dev)  # DesyncDetected: owner vs replica checksums
     gathers = [0]
 
-    def chunks(t0, t1, final_report=False):
+    def chunks(t0, t1, final_report=False, batch=None):
         """Ticks [t0, t1) as native multi-tick calls of at most --ticks-per-launch
         ticks (one steady_kernel launch each once past the first cd+1 ticks),
         split further at desync-report points: (input slice, steady, report after).
@@ -688,7 +703,7 @@ def main():
             report = world > 1 and ((every and t % args.report_interval == 0) or (final_report and t == t1))
             # each call prepared ahead (session.prepare_ticks): inside the loop only the native
             # rb_run_ticks call runs, as in a compiled host
-            call, check = sess.prepare_ticks(dinputs[t - n:t])
+            call, check = (batch or sess).prepare_ticks(dinputs[t - n:t])
             out.append((call, check, steady, report))
         return out
 
@@ -718,12 +733,21 @@ def main():
     with torch.cuda.stream(stream):
         warm_plan = chunks(0, warm)
         timed_plan = chunks(warm, warm + args.steps, final_report=True)
-        # the warmup takes the timed region's exact path (profiling events around every fused
-        # launch), so no first-call cost of that path lands inside the timed region
-        sess.profile_enable(True)
+        # the warmup takes the timed region's exact path (with GGRS_BENCH_EVENTS=launch, profiling
+        # events around every fused launch), so no first-call cost of that path lands inside it
+        sess.profile_enable(timing == "launch")
         run(warm_plan)
         torch.cuda.synchronize()
         sess.profile_take()
+        if twin is not None:  # the twin: same warmup, then the timed region's ticks with events
+            twin_plan = chunks(warm, warm + args.steps, batch=twin)
+            twin.profile_enable(True)
+            for call, check, _, _ in chunks(0, warm, batch=twin):
+                st = call()
+                if st:
+                    check(st)
+            torch.cuda.synchronize()
+            twin.profile_take()
         if world > 1:
             dist.barrier()
             torch.cuda.synchronize()
@@ -751,6 +775,20 @@ def main():
                   f"elapsed {1e6 * elapsed:.1f} us, GPU marker to marker {1e3 * ev_a.elapsed_time(ev_b):.1f} us",
                   file=sys.stderr, flush=True)
         kernel_ms, timed_ticks = sess.profile_take()  # HIP events around every steady_kernel launch
+        if twin is not None:  # the twin's launches of the same ticks, each timed by its own events
+            for call, check, _, _ in twin_plan:
+                st = call()
+                if st:
+                    check(st)
+            torch.cuda.synchronize()
+            kernel_ms, timed_ticks = twin.profile_take()
+            fr = sess.current_frame() - 1  # the newest saved cell of both batches
+            same = twin.current_frame() == fr + 1 and all(
+                (x == y).all() for x, y in zip(twin.read_cell(fr), sess.read_cell(fr)))
+            twin.close()
+            if not same:
+                raise SystemExit("twin batch diverged from the timed batch")
+            sess.profile_enable(True)
         gather_ms = [a.elapsed_time(b) for a, b in gather_ev]
         # The 60 Hz serving path, after (outside) the timed region: inputs arrive one tick at a
         # time (ex_game_synctest.rs:50-61), so each tick is its own call and launch.

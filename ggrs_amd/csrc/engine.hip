@@ -19,6 +19,7 @@
 //   live  [NW planes][Spad]   live game state between ticks when no LoadGameState follows
 //   err   [Spad] i32          MismatchedChecksum{frame}, NULL_FRAME when healthy
 //   frozen[Spad/64] u64       sessions whose advance_frame returns Err (they no longer advance)
+#include <algorithm>
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -147,6 +148,7 @@ struct rb_batch {
   // call fails with RB_PANIC, as the reference process would have stopped.
   std::string poisoned;
   bool pipe = false;  // fused steady ticks with two ticks in flight (RB_STEADY_PIPE=1 at create; A/B, tests)
+  uint32_t simds = 1024;  // SIMDs of the device (MI355X: 256 CUs x 4)
   uint32_t lds_pad = 0;  // RB_LDS_PAD (bytes) at create: dynamic LDS reserved per steady workgroup (A/B)
 };
 
@@ -335,7 +337,9 @@ rb_status rb_synctest_create(const rb_config* cfg, rb_batch** out) {
   b->W = cfg->max_prediction;
   b->P = cfg->num_players;
   b->block = cfg->block_size ? static_cast<int>(cfg->block_size) : 256;
-  if (const char* env = std::getenv("RB_LDS_PAD")) b->lds_pad = static_cast<uint32_t>(std::atoi(env));
+#if RB_EXPERIMENTS  // (A/B builds only: the knob measured no effect, round 4)
+  if (const char* env = std::getenv("RB_LDS_PAD")) b->lds_pad = static_cast<uint32_t>(std::clamp(std::atoi(env), 0, 64 * 1024));
+#endif
 #if RB_EXPERIMENTS  // steady_pipe_kernel exists in A/B builds only
   if (const char* env = std::getenv("RB_STEADY_PIPE")) b->pipe = std::atoi(env) != 0;
 #endif
@@ -358,6 +362,9 @@ rb_status rb_synctest_create(const rb_config* cfg, rb_batch** out) {
     if (_e != hipSuccess) return hip_fail(_e, #expr); \
   } while (0)
   HIP_CREATE(hipSetDevice(b->device));
+  int cus = 0;
+  HIP_CREATE(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, b->device));
+  b->simds = 4 * cus;  // 4 SIMDs per CU (CDNA)
   HIP_CREATE(hipStreamCreateWithFlags(&b->own_stream, hipStreamNonBlocking));
   b->stream = b->own_stream;
   const size_t Sp = b->Spad, NW = b->ops->nw, W = b->W, L = b->ops->lanes, Gp = Sp * L;
@@ -558,6 +565,7 @@ rb_status launch_steady_run(rb_batch* b, const uint8_t* tick_inputs, int64_t str
   r.debug = b->cfg.reserved[0];
   r.pipe = b->pipe ? 1 : 0;
   r.lds_pad = b->lds_pad;
+  r.many_waves = static_cast<uint64_t>(b->Spad) * b->ops->lanes > 2ull * 64ull * b->simds ? 1u : 0u;
   const bool timed = b->prof;
   LaunchEv ev;  // the kernel's own start / end (hipExtLaunchKernel), no marker packets around it
   if (timed) {

@@ -59,13 +59,13 @@ namespace rb {
 #define RB_PRIO_ROTATE 1  // 0: two-level turns whatever the waves per SIMD (A/B builds)
 #endif
 // The turn key: the wave's slot on its SIMD (HW_ID bits 1:0) and, in bit 2, whether the launch
-// puts more than two waves on a SIMD (1,024 SIMDs on MI355X).  Two waves take turns at priority
+// puts more than two waves on a SIMD (`many`: decided on the host from the device's SIMD count,
+// RunParams::many_waves).  Two waves take turns at priority
 // 1 over 0; three or four rotate through priorities 0-3 (each leads a quarter of the time).
 // Measured at 131,072 sessions (4 waves per SIMD): SyncTest 8.58 us per tick rotating, 8.78 with
 // two-level turns, 8.85 without turns; P2P 7.01 / 6.76 / 7.22, so p2p_kernel keeps two levels.
-__device__ __forceinline__ uint32_t wave_turn_key() {
-  const bool many = RB_PRIO_ROTATE && gridDim.x * blockDim.x > 2u * 64u * 1024u;
-  return (__builtin_amdgcn_s_getreg(0xF804) & 3u) | (many ? 4u : 0u);  // HW_ID
+__device__ __forceinline__ uint32_t wave_turn_key(bool many = false) {
+  return (__builtin_amdgcn_s_getreg(0xF804) & 3u) | (RB_PRIO_ROTATE && many ? 4u : 0u);  // HW_ID
 }
 __device__ __forceinline__ void prio_turn(uint32_t key) {
   const uint32_t c = static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime() >> RB_PRIO_SHIFT);
@@ -390,6 +390,7 @@ struct RunParams {
   uint32_t debug;           // experiment knobs (rb_config.reserved[0]); 0 in every real run
   int32_t pipe;             // 1: two ticks in flight per lane where the game allows it (steady_pipe.hpp)
   uint32_t lds_pad;         // dynamic LDS bytes per workgroup the launch reserves (unused: caps workgroups per CU)
+  uint32_t many_waves;      // the launch puts more than two waves on a SIMD of this device (prio_turn)
 };
 
 // An empty asm that reads v: the compiler must complete the load that
@@ -558,7 +559,7 @@ steady_kernel(const RunParams p) {
   settle(newin);
   if constexpr (G::kDisplay) settle(pc);
 #if RB_STEADY_PRIO
-  const uint32_t wslot = wave_turn_key();
+  const uint32_t wslot = wave_turn_key(p.many_waves != 0);
 #endif
   for (int t = 0; t < p.T; ++t) {
     const int c = p.c0 + t;
@@ -576,6 +577,9 @@ steady_kernel(const RunParams p) {
     CsCtx ctx{p.seed, s, nonce};
     int32_t mismatch = kNullFrame;
     CS recorded{};
+    // the save of this tick whose frame is a multiple of 100 (ex_game's CHECKSUM_PERIOD), if any:
+    // one scalar modulo per tick instead of a divisibility test per save
+    [[maybe_unused]] const int kp = G::kDisplay ? (100 - f0 % 100) % 100 : -1;
     uint32_t wn[NW];  // next tick's LoadGameState(c+1-CD), loaded right after this tick saves it
     // The tick's steps, instantiated twice: with the game's out-of-line range
     // checks compiled out when the whole wave's loaded state is in range
@@ -611,7 +615,7 @@ steady_kernel(const RunParams p) {
         }
         // ex_game periodic_checksum (frame % CHECKSUM_PERIOD == 0, ex_game.rs:104-111): the state an
         // AdvanceFrame reaches at frame f is the one this save checksums, so the value is this one
-        if constexpr (G::kDisplay) pc = (f % 100 == 0) ? cval : pc;
+        if constexpr (G::kDisplay) pc = (k == kp) ? cval : pc;
         // Same lane, same address, program order: this load returns the cell just stored.
         if (k == 1 && more)
           load_words<NW>(p.snap + slot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), wn);

@@ -98,7 +98,10 @@ struct InputAlphabet<G, std::void_t<decltype(G::kInputAlphabet)>> {
 // newest first (the reference's prediction, repeat-last, input_queue.rs:126-140,
 // is candidate 0) — the player's queue keeps them as a move-to-front list of
 // its 16 most recent distinct inputs, updated as each input is added (mtf_push),
-// so picking the candidates reads no input history — then, while the queue has
+// so picking the candidates reads no input history (the list is kept only by
+// launches that speculate, kSpec && kMtf: a batch whose launches do not
+// speculate — peers' connect-status reports on, kernels.hpp launch_p2p — never
+// speculates later, so no stale list is ever read) — then, while the queue has
 // seen fewer than K distinct values, the smallest values not yet taken.  Packed
 // 4 per word, unused slots 0xFF.  For the in-kernel fan-out, whose branches are
 // input classes (InputCanon), the list holds classes (DevQueue::mcanon) and the
@@ -1460,7 +1463,9 @@ p2p_kernel(const P2PParams p) {
   int32_t up_n[PPL];
   uint32_t lin_n[PPL], rv_n[PPL][kPre];
   [[maybe_unused]] PkHead pre_n[PPL];  // kWire: the next tick's packet heads
-  [[maybe_unused]] int32_t pk_ds = kWireNothing;  // kWire: the last tick's decode status of this lane's endpoint
+  [[maybe_unused]] int32_t pk_ds[PPL];  // kWire: the last tick's decode status of each endpoint this lane serves
+#pragma unroll
+  for (int j = 0; j < PPL; ++j) pk_ds[j] = kWireNothing;
   uint32_t n_thr = 0;                             // PredictionThreshold ticks of this session in the launch
   // The tick's opening, through the PredictionThreshold decision: 0 = the
   // session stopped on a panic, 1 = the tick is over (Err(PredictionThreshold)),
@@ -1487,7 +1492,7 @@ p2p_kernel(const P2PParams p) {
       if constexpr (kWire) {
         if (h < P && !((p.local_mask >> h) & 1u)) {
           const int32_t ds = wire_poll(j, h, t);
-          pk_ds = ds;  // (stored once, at the end of the launch)
+          pk_ds[j] = ds;  // (stored once per endpoint, at the end of the launch)
           // the reference panics: "decoding failed" (protocol.rs:656) or the gap assert (:639-642)
           if (ds == kWirePanic || ds == kWireGap) status = kP2PStatusPanic;
         }
@@ -1979,7 +1984,7 @@ p2p_kernel(const P2PParams p) {
 #pragma unroll
       for (int j = 0; j < PPL; ++j) {
         const int h = player_of(j);
-        if (h < P && !((p.local_mask >> h) & 1u)) p.pk_status[static_cast<size_t>(h) * p.S + s] = pk_ds;
+        if (h < P && !((p.local_mask >> h) & 1u)) p.pk_status[static_cast<size_t>(h) * p.S + s] = pk_ds[j];
       }
     }
     if (p.acks) {

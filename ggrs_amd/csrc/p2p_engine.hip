@@ -439,7 +439,6 @@ rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs,
     }
     e0 = b->prof_ev[b->prof_used].first;
     e1 = b->prof_ev[b->prof_used].second;
-    ++b->prof_used;
   }
   const bool one_launch = !b->fanout || (b->ops->inlane_fanout && !b->fan_generic);
   hipError_t e = hipSuccess;
@@ -461,6 +460,7 @@ rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs,
   }
   if (e != hipSuccess) return pfail(b, RB_DEVICE_ERROR, std::string("p2p launch: ") + hipGetErrorString(e));
   if (e1 && !one_launch) P2P_TRY(b, hipEventRecord(e1, b->stream));
+  if (e0) ++b->prof_used;  // only a launch that went out has its event pair recorded
   return RB_OK;
 }
 
@@ -500,10 +500,10 @@ rb_status rb_p2p_run_ticks_packets(rb_p2p* b, int32_t n_ticks, const void* local
       b->prof_ev.emplace_back(e0, e2);
     }
     ev = LaunchEv{b->prof_ev[b->prof_used].first, b->prof_ev[b->prof_used].second};
-    ++b->prof_used;
   }
   hipError_t e = b->ops->launch_p2p(p, b->block, b->stream, ev);
   if (e != hipSuccess) return pfail(b, RB_DEVICE_ERROR, std::string("p2p launch: ") + hipGetErrorString(e));
+  if (ev.start) ++b->prof_used;  // only a launch that went out has its event pair recorded
   return RB_OK;
 }
 

@@ -156,3 +156,43 @@ def test_gpu_plugin_p2p_matches_oracle_every_tick(gpu_available, mask, sparse, l
             np.testing.assert_array_equal(cs[v], ocs[v])
     assert rolled
     sess.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ticks_per_call", [1, 30], ids=["live", "fused"])
+def test_gpu_plugin_packet_decode_status_per_endpoint(gpu_available, ticks_per_call):
+    # One lane serves all three players of the plug-in game (two remote endpoints per lane): a bad
+    # packet from one endpoint must be reported for that endpoint only (UdpProtocol::on_input is
+    # per endpoint, protocol.rs:616-689), the other endpoint's status stays its own decode result.
+    import torch
+
+    from ggrs_amd import _lib as L
+    from test_wire import _encode_schedule
+    lib = L.load()
+    gid = register_game_plugin(PLUGIN)
+    S, T, W, mask, rd, stride = 96, 60, 8, 0b001, 1, 32
+    inputs, upto, rin = synth_network(S, P, T, mask, rd, 1, 4, mask=0x1F)
+    b = (G.SessionBuilder(gid, num_sessions=S).with_num_players(P).with_max_prediction_window(W)
+         .with_input_delay(1).with_remote_input_delay(rd))
+    for h in range(P):
+        b.add_player(PlayerType.Local if (mask >> h) & 1 else PlayerType.Remote, h)
+    wired = b.start_p2p_session()
+    di, dr = torch.from_numpy(inputs).cuda(), torch.from_numpy(rin).cuda()
+    pk, ln, st = _encode_schedule(lib, P, S, T, mask, rd, upto, dr, stride, seed=5)
+    bad_t, a_s, b_s = 30, 11, 40
+    k = int(ln[bad_t, 1, a_s])
+    assert k > 0 and int(ln[bad_t, 2, a_s]) > 0 and int(ln[bad_t, 2, b_s]) > 0
+    pk[bad_t, 1, a_s, k - 1] |= 0x80                  # endpoint 1 of session a: truncated varint (-1)
+    st[bad_t, 2, b_s] = upto[bad_t - 1, 2, b_s] + 2   # endpoint 2 of session b: skips a frame (-2)
+    dstat = torch.zeros((P, S), dtype=torch.int32, device="cuda")
+    t = 0
+    while t < T:
+        n = min(ticks_per_call, T - t)
+        wired.run_ticks_packets(di[t:t + n], pk[t:t + n], ln[t:t + n], st[t:t + n], dstat)
+        t += n
+    d = dstat.cpu().numpy()
+    assert d[1, a_s] == -1 and d[2, b_s] == -2, (d[:, a_s], d[:, b_s])
+    assert d[2, a_s] >= 0 and d[1, b_s] >= 0, (d[:, a_s], d[:, b_s])  # the good endpoint of each
+    status = wired.status()[0]
+    assert status[a_s] == 101 and status[b_s] == 101 and wired.counters()[2] == 2
+    wired.close()

@@ -55,14 +55,30 @@ __device__ __forceinline__ void op1(float& f, double& d, uint32_t& u, uint64_t& 
   if constexpr (OP == 22) asm volatile("s_nop 0" : "+v"(u));
   if constexpr (OP == 23) asm volatile("v_med3_f32 %0, %0, %1, %2" : "+v"(f) : "v"(a), "v"(a));
   if constexpr (OP == 24) asm volatile("v_max_f32 %0, %0, %1" : "+v"(f) : "v"(a));
+  if constexpr (OP == 25) asm volatile("v_mul_f32 %0, %0, %1" : "+v"(f) : "v"(a));
+  if constexpr (OP == 26) asm volatile("v_add_f32 %0, %0, %1" : "+v"(f) : "v"(a));
+  if constexpr (OP == 27) asm volatile("v_and_b32 %0, %0, %1" : "+v"(u) : "v"(ua));
+  if constexpr (OP == 28) asm volatile("v_mov_b32 %0, %1" : "=v"(u) : "v"(ua));
+  if constexpr (OP == 29) asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(q) : "v"(q));
+  if constexpr (OP == 30) asm volatile("v_mad_u32_u24 %0, %0, %1, %1" : "+v"(u) : "v"(ua));
+  if constexpr (OP == 31) asm volatile("v_perm_b32 %0, %0, %1, %1" : "+v"(u) : "v"(ua));
+  if constexpr (OP == 32) asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(f) : "v"(a), "s"(a));
+  if constexpr (OP == 33) asm volatile("v_lshlrev_b32 %0, 3, %0" : "+v"(u));
+  if constexpr (OP == 34) asm volatile("v_add_u32 %0, %0, %1" : "+v"(u) : "s"(ua));
+  if constexpr (OP == 35) asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(d) : "v"(da), "s"(da));
+  if constexpr (OP == 36) asm volatile("v_cvt_f32_f64 %0, %1\n\tv_fma_f32 %2, %3, %3, %2" : "=v"(f), "+v"(d), "+v"(u) : "v"(a));
+  if constexpr (OP == 37) asm volatile("v_fma_f64 %0, %2, %2, %0\n\tv_fma_f32 %1, %3, %3, %1" : "+v"(d), "+v"(f) : "v"(da), "v"(a));
+  if constexpr (OP == 38) asm volatile("s_add_u32 s40, s40, 1\n\tv_fma_f32 %0, %1, %1, %0" : "+v"(f) : "v"(a) : "s40");
 }
 static const char* kNames[] = {"v_fma_f32",     "v_fma_f64",      "v_mul_f64",     "v_cvt_f32_f64",  "v_cvt_f64_f32",
                                "v_cvt_i32_f64", "v_dot4_u32_u8",  "v_cndmask_b32", "v_sqrt_f32",     "v_rcp_f32",
                                "v_pk_fma_f32",  "v_add_u32",      "v_mul_hi_u32",  "v_lshl_add_u64", "v_add_u32_dpp",
                                "v_add_f64",     "v_cmp_gt_f32",   "v_div_fmas_f32", "v_cvt_f64_i32",
                                "cndmask_sgpr",  "cmp+nop1+cndmask", "v_bfi_b32",    "s_nop 0",        "v_med3_f32",
-                               "v_max_f32"};
-constexpr int kOps = 25;
+                               "v_max_f32",     "v_mul_f32",      "v_add_f32",     "v_and_b32",      "v_mov_b32",
+                               "v_pk_mul_f32",  "v_mad_u32_u24",  "v_perm_b32",    "v_fma_f32 sgpr", "v_lshlrev_b32",
+                               "v_add_u32 sgpr", "v_fma_f64 sgpr", "cvt_f32_f64+fma_f32", "fma_f64+fma_f32", "s_add+fma_f32"};
+constexpr int kOps = 39;
 
 template <int OP, int C>
 __global__ void __launch_bounds__(256) ubench(uint64_t* out, float seed) {

@@ -17,7 +17,8 @@ from ggrs_amd import _lib  # noqa: E402
 
 S = int(os.environ.get("S", 65536))
 TPL = int(os.environ.get("TPL", 50))
-T, W0 = 32 + 3 * TPL, 32
+W0 = int(os.environ.get("W0", 32))
+T = W0 + 3 * TPL
 inputs = torch.from_numpy(G.synth_inputs(S, 2, T)).cuda()
 s = (G.SessionBuilder(G.Game.EX_GAME, num_sessions=S).with_check_distance(7).with_input_delay(2)
      .with_checked_mismatches(False).start_synctest_session())
