@@ -357,39 +357,31 @@ def bench_p2p(args):
          .with_block_size(args.block_size).with_speculative_fanout(args.fanout, K))
     for h in range(P):
         b.add_player(PlayerType.Local if (mask >> h) & 1 else PlayerType.Remote, h)
-    sess = b.start_p2p_session()
     stream = torch.cuda.Stream(device=dev)
-    sess.set_stream(stream)
+    # Timing (as the SyncTest path, GGRS_BENCH_EVENTS): by default the timed region launches without
+    # events and a twin batch, built and fed identically, times the same ticks' launches afterwards.
+    timing = os.environ.get("GGRS_BENCH_EVENTS", "twin")
+    if timing not in ("twin", "launch"):
+        raise SystemExit("GGRS_BENCH_EVENTS: twin or launch")
+
+    def new_batch():
+        x = b.start_p2p_session()
+        x.set_stream(stream)
+        return x
+
+    sess = new_batch()
+    twin = new_batch() if timing == "twin" else None
     tpl = args.ticks_per_launch
-    if args.wire:  # the remote inputs travel as packets: no delivery tensors on the receiver
-        import ctypes
-        lib = G._lib.load()
-        F = dr.shape[0]
-        stride = 32
-        pk = torch.zeros((1, P, S, stride), dtype=torch.uint8, device=dev)
-        ln, st = (torch.zeros((1, P, S), dtype=torch.int32, device=dev) for _ in range(2))
-        acks = torch.full((P, S), -1, dtype=torch.int32, device=dev)  # the receiver's newest frame per endpoint
-        ptr = lambda t: ctypes.c_void_p(t.data_ptr())
-        sp = ctypes.c_void_p(stream.cuda_stream)
-        remotes = [h for h in range(P) if not (mask >> h) & 1]
-        # every call's arguments built ahead (a compiled host's loop): per tick, each remote peer's
-        # send_pending_output since its last ack (device encode), then one launch that decodes the
-        # packets inside the tick's poll and runs the tick (rb_p2p_run_ticks_packets)
-        enc_args = [[(local, sp, h, P, S, 1, ptr(dr), F, args.remote_delay, ptr(acks[h]), ptr(du[t, h]), ptr(pk[0, h]),
-                      stride, ptr(ln[0, h]), ptr(st[0, h])) for h in remotes] for t in range(T)]
-        lstride = P * S * di.element_size()
-        tick_args = [(sess._h, 1, ptr(di[t]), lstride, ptr(pk), stride, ptr(ln), ptr(st), None, ptr(acks))
-                     for t in range(T)]
-        enc, tick_fn = lib.rb_encode_input_packets, lib.rb_p2p_run_ticks_packets
+    import ctypes
+    lib = G._lib.load()
+    ptr = lambda t: ctypes.c_void_p(t.data_ptr())
+    sp = ctypes.c_void_p(stream.cuda_stream)
+    F = dr.shape[0]
+    lstride = P * S * di.element_size()
+    stride = 32
     if args.wire_replay:  # received traffic replayed: every tick's packets encoded ahead (untimed)
-        import ctypes
-        lib = G._lib.load()
-        F = dr.shape[0]
-        stride = 32
-        pk = torch.zeros((T, P, S, stride), dtype=torch.uint8, device=dev)
-        ln, st = (torch.zeros((T, P, S), dtype=torch.int32, device=dev) for _ in range(2))
-        ptr = lambda t: ctypes.c_void_p(t.data_ptr())
-        sp = ctypes.c_void_p(stream.cuda_stream)
+        rpk = torch.zeros((T, P, S, stride), dtype=torch.uint8, device=dev)
+        rln, rst = (torch.zeros((T, P, S), dtype=torch.int32, device=dev) for _ in range(2))
         rng = np.random.default_rng(args.seed)
         with torch.cuda.stream(stream):
             none = torch.full((S,), -1, dtype=torch.int32, device=dev)
@@ -404,44 +396,75 @@ def bench_p2p(args):
                     acked = torch.where(prev < 0, prev, torch.clamp(prev - redo, min=args.remote_delay - 1))
                     acked = torch.where(acked < args.remote_delay, none, acked).contiguous()
                     assert lib.rb_encode_input_packets(local, sp, h, P, S, 1, ptr(dr), F, args.remote_delay,
-                                                       ptr(acked), ptr(du[t, h].contiguous()), ptr(pk[t, h]), stride,
-                                                       ptr(ln[t, h]), ptr(st[t, h])) == 0
+                                                       ptr(acked), ptr(du[t, h].contiguous()), ptr(rpk[t, h]), stride,
+                                                       ptr(rln[t, h]), ptr(rst[t, h])) == 0
             torch.cuda.synchronize()
-        assert int((ln < 0).sum()) == 0, "a packet did not fit its row"
-        lstride = P * S * di.element_size()
-        replay_args = [(sess._h, min(T, t + tpl) - t, ptr(di[t]), lstride, ptr(pk[t]), stride, ptr(ln[t]), ptr(st[t]),
-                        None, None) for t in range(T)]
-        tick_fn = lib.rb_p2p_run_ticks_packets
+        assert int((rln < 0).sum()) == 0, "a packet did not fit its row"
 
-    def run(t0, t1):
-        if args.wire_replay:
-            bad = 0
-            for t in range(t0, t1, tpl):
-                a = replay_args[t]
-                if a[1] != min(t1, t + tpl) - t:
-                    a = (a[0], min(t1, t + tpl) - t) + a[2:]
-                bad |= tick_fn(*a)
-            if bad:
-                raise SystemExit("wire replay: a call failed")
-            return
-        if not args.wire:
-            for t in range(t0, t1, tpl):
-                e = min(t1, t + tpl)
-                sess.run_ticks(di[t:e], du[t:e], dr)
-            return
-        bad = 0
-        for t in range(t0, t1):
-            for a in enc_args[t]:
-                bad |= enc(*a)
-            bad |= tick_fn(*tick_args[t])
-        if bad:
-            raise SystemExit("wire path: a call failed")
+    def make_run(batch):
+        """The timed loop of one batch, every native call's arguments built ahead (a compiled
+        host's loop): only the C calls run inside it."""
+        h_ = batch._h
+        if args.wire:  # the remote inputs travel as packets: no delivery tensors on the receiver
+            pk = torch.zeros((1, P, S, stride), dtype=torch.uint8, device=dev)
+            ln, st = (torch.zeros((1, P, S), dtype=torch.int32, device=dev) for _ in range(2))
+            acks = torch.full((P, S), -1, dtype=torch.int32, device=dev)  # the receiver's newest frame per endpoint
+            remotes = [h for h in range(P) if not (mask >> h) & 1]
+            # per tick, each remote peer's send_pending_output since its last ack (device encode), then
+            # one launch that decodes the packets inside the tick's poll and runs the tick
+            enc_args = [[(local, sp, h, P, S, 1, ptr(dr), F, args.remote_delay, ptr(acks[h]), ptr(du[t, h]),
+                          ptr(pk[0, h]), stride, ptr(ln[0, h]), ptr(st[0, h])) for h in remotes] for t in range(T)]
+            tick_args = [(h_, 1, ptr(di[t]), lstride, ptr(pk), stride, ptr(ln), ptr(st), None, ptr(acks))
+                         for t in range(T)]
+            enc, tick_fn = lib.rb_encode_input_packets, lib.rb_p2p_run_ticks_packets
+            keep = (pk, ln, st, acks)
 
+            def run(t0, t1):
+                bad = 0
+                for t in range(t0, t1):
+                    for a in enc_args[t]:
+                        bad |= enc(*a)
+                    bad |= tick_fn(*tick_args[t])
+                if bad:
+                    raise SystemExit("wire path: a call failed")
+        else:
+            if args.wire_replay:
+                fn = lib.rb_p2p_run_ticks_packets
+                mk = lambda t, n: (h_, n, ptr(di[t]), lstride, ptr(rpk[t]), stride, ptr(rln[t]), ptr(rst[t]), None, None)
+            else:
+                fn = lib.rb_p2p_run_ticks
+                mk = lambda t, n: (h_, n, ptr(di[t]), lstride, ptr(du[t]), ptr(dr), F)
+            keep = None
+            calls = {}
+
+            def run(t0, t1):
+                bad = 0
+                for t in range(t0, t1, tpl):
+                    n = min(t1, t + tpl) - t
+                    a = calls.get((t, n))
+                    if a is None:
+                        a = calls[(t, n)] = mk(t, n)
+                    bad |= fn(*a)
+                if bad:
+                    raise SystemExit("p2p: a call failed")
+
+            for t in range(args.warmup, T, tpl):  # the timed region's calls, built ahead
+                calls[(t, min(T, t + tpl) - t)] = mk(t, min(T, t + tpl) - t)
+        run.keep = keep
+        return run
+
+    run = make_run(sess)
     with torch.cuda.stream(stream):
-        sess.profile_enable(True)  # the warmup takes the timed path (events around every launch)
+        sess.profile_enable(timing == "launch")  # the warmup takes the timed region's path
         run(0, args.warmup)
         torch.cuda.synchronize()
         sess.profile_take()
+        if twin is not None:
+            twin_run = make_run(twin)
+            twin.profile_enable(True)
+            twin_run(0, args.warmup)
+            torch.cuda.synchronize()
+            twin.profile_take()
         a0 = sess.totals()
         if world > 1:
             dist.barrier()
@@ -454,6 +477,14 @@ def bench_p2p(args):
             torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
         kernel_ms, launches = sess.profile_take()
+        if twin is not None:  # the twin's launches of the same ticks, each timed by its own events
+            twin_run(args.warmup, T)
+            torch.cuda.synchronize()
+            kernel_ms, launches = twin.profile_take()
+            same = all((x == y).all() for x, y in zip(twin.read_cells(), sess.read_cells()))
+            twin.close()
+            if not same:
+                raise SystemExit("twin batch diverged from the timed batch")
     a1 = sess.totals()
     adv, saves, loads, selects, branch = (a1[i] - a0[i] for i in range(5))
     thr, unexpected, panics = sess.counters()

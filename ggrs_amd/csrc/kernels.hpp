@@ -877,7 +877,13 @@ struct GameOpsT final : GameOps {
       // the snapshot ring in LDS (p2p_lds_cell_bytes) for launches of many ticks: it is copied in and
       // written back whole, which short launches (the wire path's one tick per launch) do not repay;
       // with the fan-out only for the in-kernel one (fanout_kernel reads the HBM cells between ticks)
-      if (p2p_lds_cells<G>(p.W, block) && p.T >= kLdsCellsMinTicks && (!kSpec || !p.fan_generic)) {
+      // ... unless the batch puts more than two waves on a SIMD and the plain or sparse path can keep
+      // only the input ring in LDS (kQ below): the LDS cells (79 KiB per 256 threads) fit two
+      // workgroups per CU, kQ four (131,072 sessions, lag 1-4: 6.72 -> 5.25 us per tick; at 65,536
+      // sessions, two waves per SIMD, the LDS cells stay faster, 3.43 against 3.81)
+      constexpr bool kHasQ = !kSpec && !kNet && G::kLanes > 1;
+      if (p2p_lds_cells<G>(p.W, block) && p.T >= kLdsCellsMinTicks && (!kSpec || !p.fan_generic) &&
+          !(kHasQ && p.many_waves)) {
         // lane-asynchronous ticks (plain path and sparse saving) unless the batch asked for lock-step
         // ticks; the fan-out runs lock-step ticks
         auto k = (!p.sync_ticks && !kSpec) ? p2p_kernel<G, kSpec, kSparse, kNet, true, !kSpec, false, kMtf>

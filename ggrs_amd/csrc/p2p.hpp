@@ -338,6 +338,7 @@ struct P2PParams {
   uint32_t local_mask;
   int32_t sparse;
   int32_t sync_ticks;  // 1: lock-step ticks on the plain path too (no kAsync; A/B and tests)
+  int32_t many_waves;  // the batch puts more than two waves on a SIMD of this device (launch_p2p_as_m)
   DesyncParams ds;
   PeerParams peer;
   // kWire (rb_p2p_run_ticks_packets): the remote inputs arrive as the peers'
@@ -771,7 +772,13 @@ __device__ uint64_t rb_p2p_phase[8 * 4096];
 #endif
 template <class G, bool kSpec, bool kSparse, bool kNet, bool kLdsC, bool kAsync, bool kWire = false, bool kMtf = false,
           bool kQ = false>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RB_P2P_WAVES_PER_EU)))
+// kQ (the input ring alone in LDS, 32 KiB per 256 threads) is capped at 128 VGPRs: with the cells in
+// HBM four workgroups fit a CU, so batches of more than two waves per SIMD run four resident instead
+// of the LDS-cell kernel's two (kernels.hpp launch_p2p_as_m).
+// The launches that keep the cells in HBM on the plain / sparse path (kQ, and the one-tick launches
+// of live play) are capped at 128 VGPRs the same way: four waves per SIMD once a batch has them.
+__global__ void __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu((kQ || (!kLdsC && !kSpec && !kNet)) ? 4 : RB_P2P_WAVES_PER_EU)))
 p2p_kernel(const P2PParams p) {
   static_assert(!kAsync || (kLdsC && !kSpec && !kNet), "lane-asynchronous ticks: plain or sparse path, LDS cells");
   static_assert(!kWire || (!kSpec && !kSparse && !kNet && !kAsync), "packet-fed ticks: the plain lock-step path");

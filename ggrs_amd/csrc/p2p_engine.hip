@@ -15,6 +15,7 @@ struct rb_p2p {
   std::unique_ptr<GameOps> ops;
   int S = 0, Spad = 0, W = 0, P = 0, block = 256;
   int device = 0;
+  uint32_t simds = 1024;  // SIMDs of the device (MI355X: 256 CUs x 4)
   hipStream_t own_stream = nullptr, stream = nullptr;
   uint32_t* snap = nullptr;
   void* cs = nullptr;
@@ -249,6 +250,9 @@ rb_status rb_p2p_create(const rb_p2p_config* cfg, rb_p2p** out) {
     if (_e != hipSuccess) return hip_fail(_e, #expr); \
   } while (0)
   P2P_CREATE(hipSetDevice(b->device));
+  int cus = 0;
+  P2P_CREATE(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, b->device));
+  b->simds = 4 * cus;  // 4 SIMDs per CU (CDNA)
   P2P_CREATE(hipStreamCreateWithFlags(&b->own_stream, hipStreamNonBlocking));
   b->stream = b->own_stream;
   const size_t Sp = b->Spad, NW = b->ops->nw, W = b->W, L = b->ops->lanes, Gp = Sp * L;
@@ -385,6 +389,7 @@ P2PParams base_params(const rb_p2p* b) {
   p.local_mask = b->cfg.local_mask;
   p.sparse = b->cfg.sparse_saving != 0;
   p.sync_ticks = b->sync_ticks ? 1 : 0;
+  p.many_waves = static_cast<uint64_t>(b->Spad) * b->ops->lanes > 2ull * 64ull * b->simds ? 1 : 0;
   p.fan_generic = b->fan_generic ? 1 : 0;
   p.fan_k = b->cfg.fanout_candidates;
   p.spec_on = b->fanout ? 1 : 0;

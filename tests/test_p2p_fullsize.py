@@ -26,12 +26,19 @@ from oracle import oracle as O
 pytestmark = pytest.mark.gpu
 
 S_FULL = 65536
+S_GPU5 = 131072  # config 5's per-GPU share (1,048,576 sessions over 8 GPUs): four waves per SIMD
 W, D, RD, LAG = 8, 2, 2, (1, 4)
-SAMPLE = np.linspace(0, S_FULL - 1, 64).astype(np.int64)  # one session in every 1,024
 
 
-def batch(P, sparse=False, fanout=False, K=16):
-    b = (G.SessionBuilder(G.Game.EX_GAME, num_sessions=S_FULL).with_num_players(P).with_max_prediction_window(W)
+def sample_of(S):
+    return np.linspace(0, S - 1, 64).astype(np.int64)  # one session in every S / 64
+
+
+SAMPLE = sample_of(S_FULL)
+
+
+def batch(P, sparse=False, fanout=False, K=16, S=S_FULL):
+    b = (G.SessionBuilder(G.Game.EX_GAME, num_sessions=S).with_num_players(P).with_max_prediction_window(W)
          .with_input_delay(D).with_remote_input_delay(RD).with_sparse_saving_mode(sparse)
          .with_speculative_fanout(fanout, K))
     for h in range(P):
@@ -42,12 +49,13 @@ def batch(P, sparse=False, fanout=False, K=16):
 class Sample:
     """The oracle's P2PSession for the sampled sessions, driven tick by tick on the same arrays."""
 
-    def __init__(self, P, inputs, upto, rin, sparse=False):
+    def __init__(self, P, inputs, upto, rin, sparse=False, sample=SAMPLE):
         self.P = P
-        self.inputs = np.ascontiguousarray(inputs[:, :, SAMPLE])
-        self.upto = np.ascontiguousarray(upto[:, :, SAMPLE])
-        self.rin = np.ascontiguousarray(rin[:, :, SAMPLE])
-        self.orc = O.OracleP2P(O.EX_GAME, P, W, D, 0b1, len(SAMPLE), sparse_saving=sparse, remote_delay=RD)
+        self.sample = sample
+        self.inputs = np.ascontiguousarray(inputs[:, :, sample])
+        self.upto = np.ascontiguousarray(upto[:, :, sample])
+        self.rin = np.ascontiguousarray(rin[:, :, sample])
+        self.orc = O.OracleP2P(O.EX_GAME, P, W, D, 0b1, len(sample), sparse_saving=sparse, remote_delay=RD)
         self.t = 0
 
     def run_to(self, t1):
@@ -61,6 +69,7 @@ class Sample:
         return last
 
     def compare(self, sess, last, tick):
+        SAMPLE = self.sample
         ost, olf, ona, ons = last
         st, lf, na, ns = sess.status()
         for name, a, b in (("status", st, ost), ("LoadGameState frame", lf, olf), ("AdvanceFrame count", na, ona),
@@ -91,9 +100,9 @@ def assert_same_batch(a, b, what):
         np.testing.assert_array_equal(x, y, err_msg=f"{what}: frames")
 
 
-def network(P, T):
+def network(P, T, S=S_FULL):
     import torch
-    inputs, upto, rin = synth_network(S_FULL, P, T, 0b1, RD, *LAG)
+    inputs, upto, rin = synth_network(S, P, T, 0b1, RD, *LAG)
     return (inputs, upto, rin), tuple(torch.from_numpy(a).cuda() for a in (inputs, upto, rin))
 
 
@@ -112,6 +121,26 @@ def test_gpu_p2p_bench_path_at_full_size(gpu_available, sparse):
     st = sess.status()[0]
     assert ((st == 0) | (st == 1)).all()
     assert sess.totals()[2] > S_FULL, "the lagged schedule must roll sessions back"
+
+
+@pytest.mark.parametrize("sparse", [False, True], ids=["plain", "sparse"])
+def test_gpu_p2p_four_waves_per_simd_at_config5_share(gpu_available, sparse):
+    """131,072 sessions (config 5's per-GPU share) put four waves on every SIMD, so 50-tick launches
+    keep only the input ring in LDS with the cells in HBM (kernels.hpp launch_p2p_as_m, p2p_kernel kQ,
+    128 VGPRs): oracle sample after every launch, and the whole batch equals one run in one-tick
+    launches (cells and input ring in HBM)."""
+    P, T, tpl = 2, 100, 50
+    (inputs, upto, rin), (di, du, dr) = network(P, T, S=S_GPU5)
+    sess, live = batch(P, sparse=sparse, S=S_GPU5), batch(P, sparse=sparse, S=S_GPU5)
+    smp = Sample(P, inputs, upto, rin, sparse=sparse, sample=sample_of(S_GPU5))
+    for t0 in range(0, T, tpl):
+        sess.run_ticks(di[t0:t0 + tpl], du[t0:t0 + tpl], dr)
+        smp.compare(sess, smp.run_to(t0 + tpl), t0 + tpl - 1)
+    for t in range(T):
+        live.run_ticks(di[t:t + 1], du[t:t + 1], dr)
+    assert_same_batch(sess, live, "50-tick (kQ) vs one-tick launches")
+    assert sess.counters()[2] == 0 and sess.totals()[:3] == live.totals()[:3]
+    assert sess.totals()[2] > S_GPU5, "the lagged schedule must roll sessions back"
 
 
 def test_gpu_p2p_one_tick_launches_at_full_size(gpu_available):
