@@ -291,13 +291,24 @@ def rehearsal(args):
             cs = splitmix64((gid << np.uint64(20)) ^ np.uint64(f))
             if os.environ.get("GGRS_REHEARSAL_CORRUPT") and rank == 0 and A and gathers == 0:
                 cs[S] ^= np.uint64(1)
-            rep = shard.pack_reports(np.stack([cs, np.zeros_like(cs)], 1), f, np.full(S + A, -1, np.int32))
-            g = shard.gather_reports(torch.from_numpy(rep.view(np.int64).reshape(-1, shard.REPORT_WORDS).copy()))
-            mism += int(shard.count_desynced(g, world, S, A))
-            nbad, detail = shard.audit_compare(g, world, S, A)
-            audit_bad += int(nbad)
-            if first_bad is None and int(nbad):
-                first_bad = [int(x) for x in detail[0]]
+            if os.environ.get("GGRS_BENCH_REPORT", "compact") == "compact":  # 4 B per session, as the GPU path
+                rep = shard.pack_compact(cs & np.uint64(0xFFFF), f, np.full(S + A, -1, np.int32))
+                g = shard.gather_compact(torch.from_numpy(rep.copy()))
+                mism += int(shard.count_desynced_compact(g, world, S, A))
+                nbad = int(shard.audit_compare_compact(g, world, S, A))
+                if first_bad is None and nbad:
+                    rows = g.view(world, S + A)
+                    bad = (rows[:, S:] != torch.roll(rows[:, :A], shifts=-1, dims=0)).nonzero()[0].tolist()
+                    first_bad = [((bad[0] + 1) % world) * S + bad[1], f]
+            else:
+                rep = shard.pack_reports(np.stack([cs, np.zeros_like(cs)], 1), f, np.full(S + A, -1, np.int32))
+                g = shard.gather_reports(torch.from_numpy(rep.view(np.int64).reshape(-1, shard.REPORT_WORDS).copy()))
+                mism += int(shard.count_desynced(g, world, S, A))
+                nbad, detail = shard.audit_compare(g, world, S, A)
+                nbad = int(nbad)
+                if first_bad is None and nbad:
+                    first_bad = [int(x) for x in detail[0]]
+            audit_bad += nbad
             gathers += 1
     elapsed = time.perf_counter() - t0
     if rank == 0:
@@ -553,7 +564,10 @@ def bench_p2p(args):
                                                       "move-to-front list), then the smallest values",
                                         "selects": selects, "loads": loads,
                                         "select_fraction": selects / max(1, selects + loads),
-                                        "branch_frames_per_s": branch / elapsed}
+                                        "branch_frames_per_s": branch / elapsed,
+                                        "adaptive": dict(zip(("active_at_end", "window_select_fraction",
+                                                              "windows_measured", "turned_off"),
+                                                             sess.fanout_state()))}
                                        if args.fanout else None),
                        "prediction_threshold_hits": thr, "panics": panics,
                        "parallelism": f"session-sharded x{world}"},
@@ -707,7 +721,12 @@ def main():
 
     sess = new_batch()
     twin = new_batch() if timing == "twin" else None  # (the brawler's 4 GiB ring twice: 8 GiB of 288)
-    reports = torch.zeros((S + A, shard.REPORT_WORDS), dtype=torch.int64, device=dev)  # rb_checksum_report, 24 B
+    # the desync report: 4 B per session (rb_export_compact_report: 16-bit checksum + mismatch flag and
+    # delta; both bench games checksum in 16 bits), or the 24 B rb_checksum_report (GGRS_BENCH_REPORT=full)
+    compact = os.environ.get("GGRS_BENCH_REPORT", "compact") == "compact"
+    report_bytes = 4 if compact else 24
+    reports = (torch.zeros((S + A,), dtype=torch.int32, device=dev) if compact else
+               torch.zeros((S + A, shard.REPORT_WORDS), dtype=torch.int64, device=dev))
     desyncs = torch.zeros((), dtype=torch.int64, device=dev)  # sessions reporting MismatchedChecksum
     audit_bad = torch.zeros((), dtype=torch.int64, device=dev)  # DesyncDetected: owner vs replica checksums
     gathers = [0]
@@ -749,14 +768,19 @@ def main():
             steady_launches += steady
             if report:
                 f = sess.current_frame() - 1
-                sess.export_checksum_report(f, reports)
+                (sess.export_compact_report if compact else sess.export_checksum_report)(f, reports)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                gathered = shard.gather_reports(reports)  # RCCL all-gather of desync reports
+                # RCCL all-gather of desync reports
+                gathered = (shard.gather_compact if compact else shard.gather_reports)(reports)
                 e1.record()
                 gather_ev.append((e0, e1))
-                desyncs.add_(shard.count_desynced(gathered, world, S, A))  # mismatch_frame != NULL_FRAME
-                audit_bad.add_(shard.audit_compare(gathered, world, S, A, detail=False)[0])  # owner != replica
+                if compact:
+                    desyncs.add_(shard.count_desynced_compact(gathered, world, S, A))  # mismatch flag
+                    audit_bad.add_(shard.audit_compare_compact(gathered, world, S, A))  # owner != replica
+                else:
+                    desyncs.add_(shard.count_desynced(gathered, world, S, A))  # mismatch_frame != NULL_FRAME
+                    audit_bad.add_(shard.audit_compare(gathered, world, S, A, detail=False)[0])  # owner != replica
                 # (the count only: the detail list's nonzero() would stall the host inside the timed loop)
                 gathers[0] += 1
         return steady_launches
@@ -952,7 +976,9 @@ def main():
                 "mismatched_sessions": int(bad.item()),
                 "desync_reports": ({"ranks": ranks_seen, "backend": backend, "gathers": gathers[0],
                                     "interval_ticks": args.report_interval,
-                                    "allgather_ms": gather_ms, "allgather_bytes_per_rank": (S + A) * 24,
+                                    "allgather_ms": gather_ms, "allgather_bytes_per_rank": (S + A) * report_bytes,
+                                    "report": "compact 4 B (rb_export_compact_report)" if compact else
+                                              "rb_checksum_report 24 B",
                                     "mismatch_rows_seen": int(desyncs.item()),
                                     "audit_sessions_per_rank": A, "audit_compared": A * world * gathers[0],
                                     "audit_desynced": int(audit_bad.item())} if world > 1 else None),

@@ -37,6 +37,7 @@ RB_FLAG_CHECKED = 1
 RB_FLAG_LANE_PER_SESSION = 2
 RB_P2P_FLAG_FANOUT = 4
 RB_P2P_FLAG_PEER_STATUS = 8
+RB_P2P_FLAG_FANOUT_ALWAYS = 16
 RB_GAME_PLUGIN_BASE = 1000
 RB_P2P_REPORTS_PER_TAKE = 8
 RB_P2P_EVENTS_KEPT = 16
@@ -75,7 +76,8 @@ class RbP2PConfig(ctypes.Structure):
         ("block_size", ctypes.c_uint32),
         ("desync_interval", ctypes.c_int32),
         ("fanout_candidates", ctypes.c_int32),
-        ("reserved", ctypes.c_uint32 * 2),
+        ("fanout_min_select_permille", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32 * 1),
     ]
 
 
@@ -114,6 +116,8 @@ SIGNATURES = [
     ("rb_read_cell", _I32, [_P, _I32, _P, _PU64]),
     ("rb_read_live", _I32, [_P, _P, _PU64, _PI32]),
     ("rb_export_checksum_report", _I32, [_P, _I32, _P]),
+    ("rb_export_compact_report", _I32, [_P, _I32, _P]),
+    ("rb_p2p_fanout_state", _I32, [_P, _PI32, ctypes.POINTER(ctypes.c_double), _PI32, _PI32]),
     ("rb_debug_corrupt_cell", _I32, [_P, _I32, _I32, _I32, ctypes.c_uint32]),
     ("rb_debug_sincosf", _I32, [_I32, _P, _P, _P, ctypes.c_int64]),
     ("rb_debug_speed_clamp", _I32, [_I32, _P, _P, _P, _P, ctypes.c_int64]),

@@ -829,6 +829,34 @@ rb_status rb_export_checksum_report(rb_batch* b, int32_t frame, void* dev_out) {
   return RB_OK;
 }
 
+namespace rb {
+// rb_export_compact_report: 4 B per session (16-bit checksums only).
+__global__ void compact_report_kernel(const uint16_t* __restrict__ cs, const int32_t* __restrict__ err, int S,
+                                      int32_t frame, uint32_t* __restrict__ out) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= S) return;
+  const int32_t e = err[s];
+  uint32_t r = cs[s];
+  if (e != kNullFrame) r |= 0x80000000u | (static_cast<uint32_t>(min(max(frame - e, 0), 0x7FFF)) << 16);
+  out[s] = r;
+}
+
+}  // namespace rb
+
+rb_status rb_export_compact_report(rb_batch* b, int32_t frame, void* dev_out) {
+  if (b->plan_only) return fail(b, RB_INVALID_REQUEST, "plan-only batch holds no states");
+  if (b->ops->cs_bytes != 2)
+    return fail(b, RB_INVALID_REQUEST, "compact reports carry 16-bit checksums: use rb_export_checksum_report");
+  if (frame < 0 || b->plan->cell_frame[frame % b->W] != frame)
+    return fail(b, RB_INVALID_REQUEST, "no cell holds frame " + std::to_string(frame));
+  const size_t slot = static_cast<size_t>(frame % b->W);
+  hipLaunchKernelGGL(rb::compact_report_kernel, dim3((b->S + 255) / 256), dim3(256), 0, b->stream,
+                     reinterpret_cast<const uint16_t*>(static_cast<uint8_t*>(b->cs) + slot * b->Spad * 2), b->err, b->S,
+                     frame, static_cast<uint32_t*>(dev_out));
+  HIP_TRY(b, hipGetLastError());
+  return RB_OK;
+}
+
 rb_status rb_debug_corrupt_cell(rb_batch* b, int32_t session, int32_t frame, int32_t word, uint32_t xor_mask) {
   if (b->plan_only) return fail(b, RB_INVALID_REQUEST, "plan-only batch holds no states");
   if (session < 0 || session >= b->S || word < 0 || word >= b->ops->canon_words)

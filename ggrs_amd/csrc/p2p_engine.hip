@@ -41,8 +41,24 @@ struct rb_p2p {
   bool prof = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev;
   size_t prof_used = 0;
+  // the adaptive fan-out (RB_P2P_FLAG_FANOUT without _ALWAYS, include/ggrs_amd.h)
+  struct FanPolicy {
+    bool adaptive = false;
+    bool active = true;          // presimulating
+    bool open = false;           // a measurement window is open (its start sums are in host[0..1])
+    bool pending = false;        // its end sums are on their way to host[2..3] (event `ev`)
+    int32_t ticks = 0;           // ticks into the window (active) or into the pause (inactive)
+    uint32_t min_permille = 150;
+    unsigned long long* dev = nullptr;   // [4] device sums: selects, loads (window start; end)
+    unsigned long long* host = nullptr;  // [4] pinned copies
+    hipEvent_t ev = nullptr;
+    double last_frac = -1.0;
+    int32_t windows = 0, turned_off = 0;
+  } fan;
   std::string last_err;
 };
+constexpr int32_t kFanProbeTicks = 64, kFanPauseTicks = 960;
+constexpr uint64_t kFanMinRollbacks = 64;  // a window with fewer rollbacks decides nothing
 
 namespace {
 thread_local std::string g_p2p_err;
@@ -71,6 +87,9 @@ void free_all(rb_p2p* b) {
                    b->ds.ev_frame, b->ds.ev_handle, b->ds.ev_local, b->ds.ev_remote};
   for (void* q : dptrs)
     if (q) (void)hipFree(q);
+  if (b->fan.dev) (void)hipFree(b->fan.dev);
+  if (b->fan.host) (void)hipHostFree(b->fan.host);
+  if (b->fan.ev) (void)hipEventDestroy(b->fan.ev);
   if (b->peer.last) (void)hipFree(b->peer.last);
   if (b->peer.disc) (void)hipFree(b->peer.disc);
   for (auto& pr : b->prof_ev) {
@@ -92,6 +111,22 @@ rb_status read_rows(rb_p2p* b, const T* dev, size_t rows, std::vector<T>& host) 
 // disconnect_player_at_frame (p2p_session.rs:555-581) for one remote handle:
 // mark it disconnected and, if the session already simulated past its last
 // input, set disconnect_frame = last_frame + 1
+// The adaptive fan-out's measurement: selects and LoadGameStates summed over the batch into out[0..1].
+__global__ void fan_sums_kernel(const unsigned long long* __restrict__ stats, int S, int Spad,
+                                unsigned long long* __restrict__ out) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long sel = s < S ? stats[static_cast<size_t>(ST_SELECT) * Spad + s] : 0ull;
+  unsigned long long ld = s < S ? stats[static_cast<size_t>(ST_LOAD) * Spad + s] : 0ull;
+  for (int o = 32; o > 0; o >>= 1) {
+    sel += __shfl_down(sel, o, 64);
+    ld += __shfl_down(ld, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(&out[0], sel);
+    atomicAdd(&out[1], ld);
+  }
+}
+
 __global__ void p2p_disconnect_kernel(int32_t* qs, const uint8_t* mask, int32_t S, int32_t Spad, int32_t h) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= S || (mask && !mask[s])) return;
@@ -282,6 +317,13 @@ rb_status rb_p2p_create(const rb_p2p_config* cfg, rb_p2p** out) {
     P2P_CREATE(hipMalloc(&b->spec_cs, W * K * Sp * b->ops->cs_bytes));
     P2P_CREATE(hipMalloc(&b->spec_meta, SM_COUNT * Sp * 4));
     P2P_CREATE(hipMemsetAsync(b->spec_meta, 0, SM_COUNT * Sp * 4, b->stream));  // nothing valid yet
+    b->fan.adaptive = (cfg->flags & RB_P2P_FLAG_FANOUT_ALWAYS) == 0;
+    if (cfg->fanout_min_select_permille) b->fan.min_permille = cfg->fanout_min_select_permille;
+    if (b->fan.adaptive) {
+      P2P_CREATE(hipMalloc(&b->fan.dev, 4 * sizeof(unsigned long long)));
+      P2P_CREATE(hipHostMalloc(&b->fan.host, 4 * sizeof(unsigned long long)));
+      P2P_CREATE(hipEventCreateWithFlags(&b->fan.ev, hipEventDisableTiming));
+    }
   }
   // SyncLayer::new / InputQueue::new / ConnectionStatus::default: every frame NULL, current 0
   std::vector<int32_t> qs(kQsFields * Sp, kNullFrame);
@@ -403,6 +445,78 @@ P2PParams base_params(const rb_p2p* b) {
 }
 }  // namespace
 
+namespace {
+// The adaptive fan-out (include/ggrs_amd.h RB_P2P_FLAG_FANOUT_ALWAYS).  Windows of kFanProbeTicks
+// ticks back to back while presimulating; each window's select and LoadGameState sums are reduced on
+// the device into pinned memory at its end (host[2..3], event `ev`) and its start (host[0..1]: the
+// previous window's end).  A call that finds the last measurement landed decides; nothing waits.
+rb_status fan_snapshot(rb_p2p* b, int off) {
+  P2P_TRY(b, hipMemsetAsync(b->fan.dev + off, 0, 2 * sizeof(unsigned long long), b->stream));
+  hipLaunchKernelGGL(fan_sums_kernel, dim3((b->S + 255) / 256), dim3(256), 0, b->stream, b->stats, b->S, b->Spad,
+                     b->fan.dev + off);
+  P2P_TRY(b, hipGetLastError());
+  P2P_TRY(b, hipMemcpyAsync(b->fan.host + off, b->fan.dev + off, 2 * sizeof(unsigned long long),
+                            hipMemcpyDeviceToHost, b->stream));
+  return RB_OK;
+}
+rb_status fan_before(rb_p2p* b) {
+  auto& f = b->fan;
+  if (!f.adaptive) return RB_OK;
+  if (f.pending && hipEventQuery(f.ev) == hipSuccess) {
+    f.pending = false;
+    const uint64_t sel = f.host[2] - f.host[0], ld = f.host[3] - f.host[1];
+    f.windows += 1;
+    if (sel + ld >= kFanMinRollbacks) {
+      f.last_frac = static_cast<double>(sel) / static_cast<double>(sel + ld);
+      if (sel * 1000ull < static_cast<uint64_t>(f.min_permille) * (sel + ld)) {
+        f.active = false;  // a pause of kFanPauseTicks plain ticks
+        f.open = false;
+        f.ticks = 0;
+        f.turned_off += 1;
+      }
+    }
+    if (f.active) {  // the next window started at this one's end
+      f.host[0] = f.host[2];
+      f.host[1] = f.host[3];
+    }
+  }
+  if (!f.active && f.ticks >= kFanPauseTicks) {  // measure again
+    f.active = true;
+    f.open = false;
+  }
+  if (f.active && !f.open) {
+    rb_status r = fan_snapshot(b, 0);
+    if (r != RB_OK) return r;
+    f.open = true;
+    f.ticks = 0;
+  }
+  return RB_OK;
+}
+rb_status fan_after(rb_p2p* b, int32_t n) {
+  auto& f = b->fan;
+  if (!f.adaptive) return RB_OK;
+  f.ticks += n;
+  if (f.active && f.open && !f.pending && f.ticks >= kFanProbeTicks) {
+    rb_status r = fan_snapshot(b, 2);
+    if (r != RB_OK) return r;
+    P2P_TRY(b, hipEventRecord(f.ev, b->stream));
+    f.pending = true;
+    f.ticks = 0;
+  }
+  return RB_OK;
+}
+}  // namespace
+
+rb_status rb_p2p_fanout_state(rb_p2p* b, int32_t* active, double* select_fraction, int32_t* windows,
+                              int32_t* turned_off) {
+  if (!b->fanout) return pfail(b, RB_INVALID_REQUEST, "the batch has no fan-out");
+  if (active) *active = (!b->fan.adaptive || b->fan.active) ? 1 : 0;
+  if (select_fraction) *select_fraction = b->fan.last_frac;
+  if (windows) *windows = b->fan.windows;
+  if (turned_off) *turned_off = b->fan.turned_off;
+  return RB_OK;
+}
+
 rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs, int64_t local_stride,
                            const int32_t* remote_upto, const void* remote_inputs, int32_t remote_frames) {
   if (n_ticks <= 0) return RB_OK;
@@ -416,6 +530,13 @@ rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs,
   p.remote_in = static_cast<const uint8_t*>(remote_inputs);
   p.remote_frames = remote_frames;
   p.T = n_ticks;
+  if (b->fanout) {
+    P2P_TRY(b, hipSetDevice(b->device));
+    rb_status r = fan_before(b);
+    if (r != RB_OK) return r;
+  }
+  const bool spec = b->fanout && (!b->fan.adaptive || b->fan.active);
+  p.spec_on = spec ? 1 : 0;
   FanParams fp{};
   fp.status = b->status;
   fp.snap = b->snap;
@@ -445,7 +566,7 @@ rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs,
     e0 = b->prof_ev[b->prof_used].first;
     e1 = b->prof_ev[b->prof_used].second;
   }
-  const bool one_launch = !b->fanout || (b->ops->inlane_fanout && !b->fan_generic);
+  const bool one_launch = !spec || (b->ops->inlane_fanout && !b->fan_generic);
   hipError_t e = hipSuccess;
   if (one_launch) {
     // all ticks in one launch (with the in-kernel fan-out); timed by the kernel's own start / end
@@ -466,6 +587,7 @@ rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs,
   if (e != hipSuccess) return pfail(b, RB_DEVICE_ERROR, std::string("p2p launch: ") + hipGetErrorString(e));
   if (e1 && !one_launch) P2P_TRY(b, hipEventRecord(e1, b->stream));
   if (e0) ++b->prof_used;  // only a launch that went out has its event pair recorded
+  if (b->fanout) return fan_after(b, n_ticks);
   return RB_OK;
 }
 

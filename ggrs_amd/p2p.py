@@ -91,6 +91,15 @@ class P2PSession(_StreamOrdered):
         self._check(self._lib.rb_p2p_set_stream(self._h, ctypes.c_void_p(stream.cuda_stream if stream else 0)))
         self._bind(self._device, self._lib.rb_p2p_get_stream(self._h) or 0)
 
+    def fanout_state(self):
+        """The adaptive fan-out (rb_p2p_fanout_state): (active, select fraction of the last
+        measured window or -1, windows measured, times turned off)."""
+        a, w, o = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        f = ctypes.c_double()
+        self._check(self._lib.rb_p2p_fanout_state(self._h, ctypes.byref(a), ctypes.byref(f), ctypes.byref(w),
+                                                  ctypes.byref(o)))
+        return bool(a.value), f.value, w.value, o.value
+
     def run_ticks(self, local_inputs, remote_upto, remote_inputs) -> None:
         """T ticks: [poll_remote_clients, add_local_input for every local handle,
         advance_frame, handle_requests] x T in one device launch.

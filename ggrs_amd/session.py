@@ -247,13 +247,19 @@ class SessionBuilder:
         self._sparse = bool(sparse_saving)
         return self
 
-    def with_speculative_fanout(self, on: bool, candidates: int = 16) -> "SessionBuilder":
+    def with_speculative_fanout(self, on: bool, candidates: int = 16, adaptive: bool = True,
+                                min_select_permille: int = 0) -> "SessionBuilder":
         """P2P: presimulate `candidates` (1..16) candidate inputs of the
         most-lagging remote handle after every tick (RB_P2P_FLAG_FANOUT,
         BASELINE config 4): the whole input alphabet when it has at most that
-        many values (ex_game), else the most likely ones (include/ggrs_amd.h)."""
+        many values (ex_game), else the most likely ones (include/ggrs_amd.h).
+        adaptive: pause it while too few rollbacks become selects (below
+        min_select_permille, 0 = the engine's default; RB_P2P_FLAG_FANOUT_ALWAYS
+        when False)."""
         self._fanout = bool(on)
         self._fanout_k = int(candidates)
+        self._fanout_adaptive = bool(adaptive)
+        self._fanout_permille = int(min_select_permille)
         return self
 
     def with_desync_detection_mode(self, interval: int) -> "SessionBuilder":  # builder.rs:169-172
@@ -299,10 +305,12 @@ class SessionBuilder:
         pc.sparse_saving = int(getattr(self, "_sparse", False))
         pc.flags = (self._cfg.flags & L.RB_FLAG_LANE_PER_SESSION) | (
             L.RB_P2P_FLAG_FANOUT if getattr(self, "_fanout", False) else 0) | (
+            L.RB_P2P_FLAG_FANOUT_ALWAYS if not getattr(self, "_fanout_adaptive", True) else 0) | (
             L.RB_P2P_FLAG_PEER_STATUS if getattr(self, "_peer_status", False) else 0)
         pc.block_size = self._cfg.block_size
         pc.desync_interval = getattr(self, "_desync", 0)
         pc.fanout_candidates = getattr(self, "_fanout_k", 16)
+        pc.fanout_min_select_permille = getattr(self, "_fanout_permille", 0)
         h = ctypes.c_void_p()
         st = lib.rb_p2p_create(ctypes.byref(pc), ctypes.byref(h))
         if st != L.RB_OK:
@@ -568,6 +576,15 @@ class SyncTestSession(_StreamOrdered):
             self._h, img.ctypes.data_as(ctypes.c_void_p),
             dcs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), fr.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
         return img, dcs, fr
+
+    def export_compact_report(self, frame: int, dev_ptr) -> None:
+        """Write [S] uint32 compact reports (rb_export_compact_report: 16-bit checksum,
+        mismatch delta and flag) for ``frame`` to device memory; 16-bit-checksum games only."""
+        is_t = hasattr(dev_ptr, "data_ptr")
+        ptr = dev_ptr.data_ptr() if is_t else dev_ptr
+        cur = self._pre()
+        _raise(self._lib, self._h, self._lib.rb_export_compact_report(self._h, int(frame), ctypes.c_void_p(ptr)))
+        self._post(cur, (dev_ptr,) if is_t else (), outputs=True)
 
     def export_checksum_report(self, frame: int, dev_ptr: int) -> None:
         """Write [S] rb_checksum_report (24 B each) for ``frame`` to device memory

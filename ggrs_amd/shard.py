@@ -109,6 +109,61 @@ def audit_compare(gathered, world: int, owned: int, audit: int, detail: bool = T
     return bad.sum(), detail
 
 
+# ---------------------------------------------------------------------------- compact reports (4 B)
+# rb_export_compact_report: one uint32 per session, for 16-bit checksums (ex_game's fletcher16, the
+# brawler's): bits 0-15 the checksum, 16-30 the frames since the MismatchedChecksum (saturated),
+# bit 31 the mismatch flag.  The report frame is batch-uniform (every rank reports the same tick),
+# so it is not repeated per session: 4 B instead of 24 per session and all-gather.
+COMPACT_MISMATCH = 1 << 31
+
+
+def pack_compact(checksums16: np.ndarray, frame: int, mismatch_frames: np.ndarray) -> np.ndarray:
+    """Host mirror of rb_export_compact_report: [S] int32 records (the bit pattern of the uint32s)."""
+    r = checksums16.astype(np.uint32) & np.uint32(0xFFFF)
+    bad = mismatch_frames != NULL_FRAME
+    delta = np.clip(frame - mismatch_frames.astype(np.int64), 0, 0x7FFF).astype(np.uint32)
+    r = np.where(bad, r | np.uint32(COMPACT_MISMATCH) | (delta << np.uint32(16)), r)
+    return r.astype(np.uint32).view(np.int32)
+
+
+def gather_compact(local, group=None):
+    """All-gather [S] int32 compact reports from every rank: [world * S] in rank order."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    out = torch.empty((world * local.shape[0],), dtype=local.dtype, device=local.device)
+    if dist.get_backend(group) == "nccl":
+        dist.all_gather_into_tensor(out, local, group=group)  # RCCL all-gather over xGMI
+    else:
+        parts = list(out.chunk(world))
+        dist.all_gather(parts, local, group=group)
+        out = torch.cat(parts)
+    return out
+
+
+def _owned_compact(gathered, world, owned, audit):
+    if not audit:
+        return gathered
+    return gathered.view(world, owned + audit)[:, :owned].reshape(-1)
+
+
+def count_desynced_compact(gathered, world: int = 1, owned: int = 0, audit: int = 0):
+    """Sessions reporting MismatchedChecksum (bit 31 set: negative as int32)."""
+    return (_owned_compact(gathered, world, owned, audit) < 0).sum()
+
+
+def audit_compare_compact(gathered, world: int, owned: int, audit: int):
+    """audit_compare over compact reports: owner and replica records must be equal (checksum,
+    mismatch flag and delta); returns the count of disagreeing replicas as a tensor."""
+    import torch
+    if world < 2 or audit <= 0:
+        return torch.zeros((), dtype=torch.int64, device=gathered.device)
+    rows = gathered.view(world, owned + audit)
+    replica = rows[:, owned:owned + audit]
+    owner = torch.roll(rows[:, :audit], shifts=-1, dims=0)
+    return (replica != owner).sum()
+
+
 # ---------------------------------------------------------------------------- P2P ChecksumReports
 def p2p_reports_to_rows(frames: np.ndarray, checksums: np.ndarray) -> np.ndarray:
     """[K, S] frames + [K, S, 2] u128 (lo, hi) -> [K, S, 3] int64 rows in the

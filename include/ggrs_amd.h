@@ -186,6 +186,17 @@ rb_status rb_read_live(rb_batch* b, void* images, uint64_t* display_checksums, i
  * input).  Stream-ordered, does not synchronise. */
 rb_status rb_export_checksum_report(rb_batch* b, int32_t frame, void* dev_out);
 
+/* The same report in 4 bytes per session, for games whose checksum is 16 bits
+ * (ex_game's fletcher16): dev_out[S] uint32 records
+ *   bits 0-15   the checksum of the cell holding `frame` (ChecksumReport::checksum)
+ *   bits 16-30  frame - mismatch_frame, saturated at 0x7FFF (0 when healthy)
+ *   bit  31     the session reports MismatchedChecksum
+ * The report frame (ChecksumReport::frame, messages.rs:75-79) is batch-uniform in
+ * SyncTest, so it travels once per all-gather instead of once per session: the
+ * multi-GPU gather moves 4 B per session instead of 24.  RB_INVALID_REQUEST for a
+ * game with a wider checksum (use rb_export_checksum_report).  Stream-ordered. */
+rb_status rb_export_compact_report(rb_batch* b, int32_t frame, void* dev_out);
+
 /* Fault injection for tests: XOR `xor_mask` into state word `word` of
  * `session` in the cell holding `frame` (a corrupted snapshot makes the next
  * resimulation diverge, which SyncTest must report). */
@@ -250,7 +261,10 @@ typedef struct rb_p2p_config {
   int32_t desync_interval; /* with_desync_detection_mode (builder.rs:167-172): DesyncDetection::On{interval}
                               for interval > 0, Off for 0 (the default, builder.rs:15) */
   int32_t fanout_candidates; /* RB_P2P_FLAG_FANOUT: branches per session, 1..16 (default 16) */
-  uint32_t reserved[2];
+  uint32_t fanout_min_select_permille; /* adaptive fan-out (RB_P2P_FLAG_FANOUT without _ALWAYS): the
+                              select fraction of rollbacks below which the batch turns it off;
+                              0 = the default, 150 */
+  uint32_t reserved[1];
 } rb_p2p_config;
 
 /* Speculative branch fan-out (BASELINE config 4): after every tick each session
@@ -270,6 +284,17 @@ typedef struct rb_p2p_config {
  * between one-tick P2P launches); not with sparse saving. */
 #define RB_P2P_FLAG_FANOUT 4u
 
+/* The fan-out is adaptive by default: a batch measures, over windows of 64
+ * ticks, the fraction of its rollbacks that became selects; below
+ * fanout_min_select_permille it stops presimulating for the next 960 ticks (its
+ * ticks run as plain P2P ticks), then measures again.  Presimulation only pays
+ * through selects: a stream whose held inputs rarely match a candidate (the
+ * brawler's 256-value inputs: 3.8% of rollbacks at 20x the plain tick's cost)
+ * gets plain rollback.  The measurement is asynchronous (a device reduction into
+ * pinned memory, read when it has landed): no call waits for it.  Results are
+ * the same either way.  RB_P2P_FLAG_FANOUT_ALWAYS keeps it on. */
+#define RB_P2P_FLAG_FANOUT_ALWAYS 16u
+
 /* Peers' connect-status reports (update_player_disconnects, p2p_session.rs:707-742):
  * every advance_frame combines what the running endpoints last reported about
  * each player (rb_p2p_receive_peer_connect_status) with the session's own
@@ -279,6 +304,13 @@ typedef struct rb_p2p_config {
 
 /* SessionBuilder::new() defaults for a 2-player session, handle 0 local, handle 1 remote. */
 void rb_p2p_config_init(rb_p2p_config* cfg);
+
+/* The adaptive fan-out's state: *active (1: presimulating), the select fraction of
+ * rollbacks of the last measured window (-1: none yet), the windows measured and
+ * the times it was turned off.  Does not synchronise.  RB_INVALID_REQUEST without
+ * the fan-out. */
+rb_status rb_p2p_fanout_state(rb_p2p* b, int32_t* active, double* select_fraction, int32_t* windows,
+                              int32_t* turned_off);
 
 /* SessionBuilder::start_p2p_session (builder.rs:251-308) for S sessions that
  * start Running (the synchronisation handshake is the network's). */

@@ -56,6 +56,13 @@ def _drive(orc, plan, inputs, t, victim_local):
             assert [(int(r.kind), r.frame) for r in reqs] == orc.trace(0)
 
 
+def _compact_for(orc, frame):
+    frames, _, _, cs = orc.read_cells()
+    w = int(np.nonzero(frames == frame)[0][0])
+    k, f = orc.last_errors
+    return shard.pack_compact(cs[w][:, 0], frame, np.where(k == 3, f, -1).astype(np.int32))
+
+
 def _rank_main(rank, world, port, outdir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -68,7 +75,7 @@ def _rank_main(rank, world, port, outdir):
         plan = (G.SessionBuilder(G.Game.EX_GAME, num_sessions=hi - lo, device=-1).with_num_players(P)
                 .with_check_distance(CD).with_input_delay(DELAY).start_synctest_session())
         victim = VICTIM - lo if lo <= VICTIM < hi else None
-        gathered_all = []
+        gathered_all, compact_all = [], []
         for t in range(T):
             _drive(orc, plan, inputs, t, victim)
             if orc.current_frame() % INTERVAL == 0:
@@ -78,7 +85,13 @@ def _rank_main(rank, world, port, outdir):
                 gathered_all.append(g.numpy())
                 bad = shard.desynced_sessions(g).tolist()
                 assert bad == ([VICTIM] if t >= 15 else []), (t, bad)
+                # the compact form (rb_export_compact_report): 4 B per session, same verdict
+                c = shard.gather_compact(torch.from_numpy(_compact_for(orc, orc.current_frame() - 1)))
+                compact_all.append(c.numpy())
+                assert int(shard.count_desynced_compact(c)) == (1 if t >= 15 else 0)
+                assert ((c.numpy() < 0).nonzero()[0].tolist()) == ([VICTIM] if t >= 15 else [])
         np.save(os.path.join(outdir, f"rank{rank}.npy"), np.stack(gathered_all))
+        np.save(os.path.join(outdir, f"compact{rank}.npy"), np.stack(compact_all))
     finally:
         dist.destroy_process_group()
 
@@ -101,13 +114,45 @@ def test_report_layout_matches_abi():
     assert w[0] == 5 and w[1] == 7 and (w[2] >> 32) == -1 and (w[2] & 0xFFFFFFFF) == 42
 
 
+def test_compact_report_layout():
+    # rb_export_compact_report's record: checksum in bits 0-15, frames since the mismatch in 16-30
+    # (saturated), the MismatchedChecksum flag in bit 31
+    r = shard.pack_compact(np.array([0xBEEF, 0x1234, 7, 9], np.uint64), 100,
+                           np.array([-1, 97, 100, -50000], np.int32)).view(np.uint32)
+    assert r[0] == 0xBEEF
+    assert r[1] == 0x80000000 | (3 << 16) | 0x1234
+    assert r[2] == 0x80000000 | 7
+    assert r[3] == 0x80000000 | (0x7FFF << 16) | 9
+
+
+def test_audit_compare_compact_finds_the_corrupted_replica():
+    world, owned, audit = 3, 8, 4
+    rows = np.arange(world * (owned + audit), dtype=np.int32).reshape(world, owned + audit)
+    for r in range(world):  # each rank's replicas = the next rank's first `audit` owned records
+        rows[r, owned:] = rows[(r + 1) % world, :audit]
+    g = torch.from_numpy(rows.reshape(-1).copy())
+    assert int(shard.audit_compare_compact(g, world, owned, audit)) == 0
+    rows[1, owned + 2] ^= 1  # rank 1's replica of rank 2's session 2
+    assert int(shard.audit_compare_compact(torch.from_numpy(rows.reshape(-1).copy()), world, owned, audit)) == 1
+    rows[0, 3] |= np.int32(-2 ** 31)  # a mismatch flag on an owned session
+    assert int(shard.count_desynced_compact(torch.from_numpy(rows.reshape(-1).copy()), world, owned, audit)) == 1
+
+
 def test_two_rank_gloo_report_allgather_equals_single_process():
     port = _free_port()
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_rank_main, args=(2, port, d), nprocs=2, join=True)
         r0 = np.load(os.path.join(d, "rank0.npy"))
         r1 = np.load(os.path.join(d, "rank1.npy"))
+        c0 = np.load(os.path.join(d, "compact0.npy"))
+        c1 = np.load(os.path.join(d, "compact1.npy"))
     np.testing.assert_array_equal(r0, r1)  # every rank sees the same node-wide reports
+    np.testing.assert_array_equal(c0, c1)
+    # the compact records carry exactly the full reports' low 16 checksum bits and mismatch flag
+    lo16 = (r0[..., 0] & 0xFFFF).astype(np.int64)
+    flag = (r0[..., 2] >> 32) != -1
+    np.testing.assert_array_equal(c0.astype(np.int64) & 0xFFFF, lo16)
+    np.testing.assert_array_equal(c0 < 0, flag)
     # single process over all sessions
     orc = O.OracleBatch(O.EX_GAME, P, 8, CD, DELAY, TOTAL)
     inputs = G.synth_inputs(TOTAL, P, T)

@@ -298,6 +298,22 @@ def test_gpu_rccl_world1_report_allgather_and_p2p_exchange(gpu_available):
         r = g.cpu().numpy()
         np.testing.assert_array_equal(r[:, 0].view(np.uint64), cs[w][:, 0])
         assert ((r[:, 2] & 0xFFFFFFFF) == T - 1).all() and ((r[:, 2] >> 32) == -1).all()
+        # the compact 4 B report (rb_export_compact_report) through the same collective
+        crep = torch.full((S,), 7, dtype=torch.int32, device=dev)
+        sess.export_compact_report(T - 1, crep)
+        cg = shard.gather_compact(crep)
+        assert torch.equal(cg, crep)
+        np.testing.assert_array_equal(cg.cpu().numpy(), shard.pack_compact(cs[w][:, 0], T - 1, np.full(S, -1, np.int32)))
+        # a corrupted snapshot: the next tick's resimulation mismatches, and the record says so
+        sess.debug_corrupt_cell(5, T - 7, 0, 0x100)
+        more = G.synth_inputs(S, P, T + 1)[T:T + 1]
+        sess.run_ticks(torch.from_numpy(np.ascontiguousarray(more)).to(dev))
+        mm = sess.mismatches()
+        assert mm[5] != G.NULL_FRAME and (np.delete(mm, 5) == G.NULL_FRAME).all()
+        sess.export_compact_report(T, crep)
+        c = shard.gather_compact(crep).cpu().numpy().view(np.uint32)
+        assert (c >> 31).tolist() == [1 if i == 5 else 0 for i in range(S)]
+        assert (c[5] >> 16) & 0x7FFF == T - mm[5]
         sess.close()
         # P2P ChecksumReports through the all-gather, one corrupted session
         S, T, d, interval = 96, 60, 2, 5
