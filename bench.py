@@ -224,7 +224,8 @@ def roofline_block(bytes_per_launch, avg_kernel_s, ticks_per_launch, launches, k
         r["pmc_profile"] = prof["file"]
         iss = prof.get("issue")
         if iss:
-            r["valu"] = {k: iss[k] for k in ("valu_insts_per_wave", "valu_issue_frac", "issue_stall_frac",
+            r["valu"] = {k: iss[k] for k in ("valu_insts_per_wave", "salu_insts_per_wave", "valu_issue_frac",
+                                              "issue_per_quad", "active_inst_valu_frac", "issue_stall_frac",
                                               "waves_per_simd", "waves_dispatched_per_simd", "clock_GHz_sq",
                                               "l2_hit") if k in iss}
             # against what DRAM delivers in practice: the calibrated store ceiling (5.9 TB/s), not the spec
@@ -233,6 +234,14 @@ def roofline_block(bytes_per_launch, avg_kernel_s, ticks_per_launch, launches, k
             if r["dram_frac_of_ceiling"] > 0.7:
                 r["bound"], r["limiter"] = "hbm", (f"hbm bandwidth: {r['dram_frac_of_ceiling']:.2f} of the "
                                                    f"{ceil:.0f} GB/s measured store ceiling")
+            elif iss.get("issue_per_quad", 0.0) > 0.8:
+                # SIMD instruction issue (profiles/r05_twopoint_pmc.json: doubling the resident waves moves
+                # the issue rate from 0.92 to 0.99 instructions per quad-cycle and gains 4%; issue stalls
+                # go from 21% to 54% of wave time)
+                r["bound"], r["limiter"] = "issue", (
+                    f"SIMD instruction issue: {iss['issue_per_quad']:.2f} vector + scalar instructions per "
+                    f"quad-cycle per SIMD at {iss['waves_per_simd']:.1f} waves per SIMD (dual issue is rare at "
+                    f"this mix); HBM traffic {r['dram_frac']:.2f} of peak")
             elif iss["valu_issue_frac"] > 0.7:
                 r["bound"], r["limiter"] = "valu", "valu issue"
             else:
@@ -365,7 +374,8 @@ def bench_p2p(args):
     b = (G.SessionBuilder(G.Game.BRAWLER if brawler else G.Game.EX_GAME, num_sessions=S, device=local)
          .with_num_players(P).with_max_prediction_window(W).with_input_delay(args.input_delay)
          .with_remote_input_delay(args.remote_delay).with_sparse_saving_mode(args.sparse_saving)
-         .with_block_size(args.block_size).with_speculative_fanout(args.fanout, K))
+         .with_block_size(args.block_size)
+         .with_speculative_fanout(args.fanout, K, per_player=args.fanout_mode == "per-player"))
     for h in range(P):
         b.add_player(PlayerType.Local if (mask >> h) & 1 else PlayerType.Remote, h)
     stream = torch.cuda.Stream(device=dev)
@@ -528,6 +538,7 @@ def bench_p2p(args):
         avg_kernel_s = kernel_ms / 1e3 / max(1, launches)
         cfg_key = (f"p2p {args.game} P={P} W={W} d={args.input_delay} rd={args.remote_delay} lag={lo},{hi} S={S}"
                    + (" sparse" if args.sparse_saving else "") + (f" fanout{'' if K == 16 else K}" if args.fanout else "")
+                   + (" per-player" if args.fanout and args.fanout_mode == "per-player" else "")
                    + (" wire" if args.wire else "") + (" wire-replay" if args.wire_replay else ""))
         tl = int(round(args.steps / max(1, launches)))  # the PMC profile of the launch shape timed here
         cfg_key += f" tpl={tl}" if tl != 50 else ""
@@ -559,6 +570,7 @@ def bench_p2p(args):
                        "advance_frames_per_session_tick": adv / (S * world * args.steps),
                        "rollbacks_per_session_tick": (loads + selects) / (S * world * args.steps),
                        "speculative": ({"branches": K, "alphabet": 16 if not brawler else 256,
+                                        "mode": args.fanout_mode,
                                         "candidates": "whole alphabet" if (not brawler and K >= 16) else
                                                       "the K most recently added distinct inputs (the queue's "
                                                       "move-to-front list), then the smallest values",
@@ -637,6 +649,9 @@ def main():
     ap.add_argument("--fanout", action="store_true",
                     help="p2p: speculative fan-out, --fanout-k candidate inputs per session per tick (BASELINE "
                          "configs[3]; use with --num-players 4)")
+    ap.add_argument("--fanout-mode", choices=["single", "per-player"], default="single",
+                    help="p2p --fanout: speculate the remote player with the oldest unconfirmed input (single) or "
+                         "every remote player (per-player, RB_P2P_FLAG_FANOUT_PER_PLAYER; whole alphabet only)")
     ap.add_argument("--fanout-k", type=int, default=16,
                     help="p2p --fanout: candidates per session (1..16): ex_game's whole alphabet at 16, else the "
                          "most likely K")

@@ -38,6 +38,7 @@ RB_FLAG_LANE_PER_SESSION = 2
 RB_P2P_FLAG_FANOUT = 4
 RB_P2P_FLAG_PEER_STATUS = 8
 RB_P2P_FLAG_FANOUT_ALWAYS = 16
+RB_P2P_FLAG_FANOUT_PER_PLAYER = 32
 RB_GAME_PLUGIN_BASE = 1000
 RB_P2P_REPORTS_PER_TAKE = 8
 RB_P2P_EVENTS_KEPT = 16

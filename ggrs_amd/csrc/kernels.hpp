@@ -795,6 +795,7 @@ struct GameOps {
   virtual hipError_t launch_fanout(const FanParams& p, int block, hipStream_t st) const = 0;
   bool fanout_supported = false;
   bool inlane_fanout = false;  // p2p_kernel runs the fan-out itself (inlane_fan), unless fan_generic
+  uint32_t input_alphabet = 0;  // InputAlphabet<G>: the per-player fan-out needs all of it as candidates
 };
 
 template <class G>
@@ -811,6 +812,7 @@ struct GameOpsT final : GameOps {
     display = G::kDisplay;
     fanout_supported = kFanout;
     inlane_fanout = kFanout && inlane_fan<G>();
+    input_alphabet = InputAlphabet<G>::value;
   }
   void word_loc(int k, int* lane, int* word) const override { G::word_loc(k, lane, word); }
   void init_words(uint32_t* w) const override { G::init(w); }

@@ -326,6 +326,7 @@ struct P2PParams {
   const void* spec_cs;   // [W][Spad][16] CS (fanout_kernel)
   int32_t* spec_meta;    // [SM_COUNT][Spad]
   int32_t spec_on;
+  int32_t spec_per_player;  // the in-kernel fan-out speculates every remote player (RB_P2P_FLAG_FANOUT_PER_PLAYER)
   int32_t fan_generic;  // the branches come from fanout_kernel (RB_FANOUT_GENERIC=1, or a game without kInFan)
   int32_t fan_k;        // candidates (branches) per session, <= kSpecBranches
   const uint8_t* local_in;  // tick t, handle h: local_in + t * local_stride + (h * S + s) * IB
@@ -886,6 +887,10 @@ p2p_kernel(const P2PParams p) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) sm_cand[q] = static_cast<uint32_t>(p.spec_meta[(SM_CAND + q) * Spad + s]);
   }
+  // per-player fan-out: this lane's player's first unconfirmed frame when its branches were made
+  // (row SM_CAND + lane: the candidate rows are free there, the candidates being the whole alphabet)
+  [[maybe_unused]] int32_t sm_pbase = 0;
+  if constexpr (kInFan && !kMtf) sm_pbase = static_cast<int32_t>(sm_cand[min(lane, 3)]);
   // ---- the per-tick delivery tensors, loaded one tick ahead: at the top of
   // tick t, before its snapshot stores, come the delivered watermark and the
   // local inputs of tick t+1; right after the poll, the first kPre remote
@@ -1110,10 +1115,102 @@ p2p_kernel(const P2PParams p) {
   // confirmed then k predicted for the speculated player, the reference's
   // predictions for the others, confirmed local inputs).  The sync layer's
   // bookkeeping runs as in adjust (dry), the cells and the state are copied.
+  // The per-player select (fan_per_player's branches): the rollback starts at their base B, and
+  // every remote player's inputs since its own base hold one class (newly confirmed ones, then the
+  // repeat-last prediction; or the prediction alone when none arrived): each lane takes its player's
+  // branch of that class (a local player: its one chain) for every cell adjust would save and for
+  // the state, and each cell's checksum is rebuilt from the players' fletcher parts.
+  // A rollback from F > B (the oldest-unconfirmed player did not mispredict; a later one did) selects
+  // too when every lane's branch word at F equals the cell of F the reference loads: the trajectories
+  // then agree from F on, whatever the cells of frames B .. F hold (a PredictionThreshold tick can
+  // leave cells computed with predictions the sync layer has since dropped, p2p_session.rs:320).
+  auto select_per_player = [&](int32_t first_incorrect, int32_t min_confirmed) __attribute__((always_inline)) -> bool {
+    if constexpr (kInFan && !kMtf) {
+      const int32_t B = sm_base;
+      if (first_incorrect < B || first_incorrect >= cur || B + W <= cur) return false;
+      const int32_t F = first_incorrect;
+      constexpr auto AC = AlphabetClasses<G>::value;
+      uint32_t acp[4];
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) acp[qq] = AC.packed[qq];
+      const bool my_remote = lane < P && !((p.local_mask >> lane) & 1u);
+      bool ok = true;
+      int32_t kk = 0;
+      if (my_remote) {
+        const int32_t la = q[0].last_added;
+        const int32_t pb = sm_pbase;  // this player's first unconfirmed frame at the branches' making
+        // the class held from pb on: the first newly confirmed input, else the prediction
+        const uint32_t c0 = InputCanon<G>::apply(la >= pb ? ring.get(pb, lane, s) : (la == kNullFrame ? 0u : ring.get(la, lane, s))) & 0xFFu;
+        for (int32_t f = pb + 1; f <= la && f < cur; ++f) ok &= (InputCanon<G>::apply(ring.get(f, lane, s)) & 0xFFu) == c0;
+        kk = cand_find(acp, c0, AC.n);
+        ok &= kk >= 0;
+      }
+      const unsigned Gs = Spad * static_cast<unsigned>(L) * static_cast<unsigned>(kSpecBranches + 1);
+      const unsigned col = my_remote ? (s * static_cast<unsigned>(L) + static_cast<unsigned>(lane)) * kSpecBranches +
+                                           static_cast<unsigned>(kk >= 0 ? kk : 0)
+                                     : Spad * static_cast<unsigned>(L) * kSpecBranches + s * L + static_cast<unsigned>(lane);
+      const bool has = lane < P;
+      if (F > B && ok && has) {  // the branch at F must be the cell the reference loads
+        const unsigned fslot = static_cast<unsigned>(F % W);
+        uint32_t bw[NW], cw[NW];
+        load_words<NW>(p.spec_cells + fslot * NW * Gs, static_cast<int>(Gs), static_cast<int>(col), bw);
+        if constexpr (kLdsC) {
+#pragma unroll
+          for (int n = 0; n < NW; ++n) cw[n] = lds_cell[(fslot * NW + n) * bd + tid];
+        } else {
+          load_words<NW>(p.snap + fslot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), cw);
+        }
+#pragma unroll
+        for (int n = 0; n < NW; ++n) ok &= bw[n] == cw[n];
+      }
+      ok = group_min<L>(ok ? 1 : 0) == 1;
+      if (!ok) return false;
+      exec = false;  // the sync layer's side of adjust_gamestate
+      adjust(first_incorrect, min_confirmed);
+      exec = true;
+      if (status == kP2PStatusPanic) return true;
+      for (int32_t f = F + 1; f < cur; ++f) {  // the cells adjust would have saved
+        const unsigned slot = static_cast<unsigned>(f % W);
+        uint32_t cw[NW] = {};
+        if (has) load_words<NW>(p.spec_cells + slot * NW * Gs, static_cast<int>(Gs), static_cast<int>(col), cw);
+        if (has) {
+          if constexpr (kLdsC) {
+#pragma unroll
+            for (int n = 0; n < NW; ++n) lds_cell[(slot * NW + n) * bd + tid] = cw[n];
+          } else {
+            store_words<NW>(p.snap + slot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), cw);
+          }
+        }
+        Fl16 a{0u, 0u};
+        if (has) a = G::fan_partial(cw, lane);
+        a.s1 = group_sum<L>(a.s1);
+        a.s2 = group_sum<L>(a.s2);
+        const CS c = G::fan_finish(a, f);
+        if (lead) {
+          if constexpr (kLdsC) {
+            lds_cs[slot * bps + sl] = c;
+            lds_tag[slot * bps + sl] = f;
+          } else {
+            csa[slot * Spad + s] = c;
+            p.tag[slot * Spad + s] = f;
+          }
+        }
+        ++tot_save;
+      }
+      if (has) load_words<NW>(p.spec_state, static_cast<int>(Gs), static_cast<int>(col), w);
+      ++tot_sel;
+      return true;
+    } else {
+      return false;
+    }
+  };
   auto try_select = [&](int32_t first_incorrect, int32_t min_confirmed) __attribute__((always_inline)) -> bool {
     if (kLdsC && !in_fan) return false;  // (not launched: fanout_kernel's branches need HBM cells)
     if (any_disc || disc_frame != kNullFrame) return false;  // the branches assumed everybody connected
     if (!(sm_valid & 1) || sm_end != cur) return false;
+    if constexpr (kInFan && !kMtf) {
+      if (sm_valid & (1 << 16)) return select_per_player(first_incorrect, min_confirmed);
+    }
     const int32_t base = sm_base;
     const int rs = sm_player;
     if (first_incorrect != base || base + W <= cur) return false;
@@ -1655,7 +1752,128 @@ p2p_kernel(const P2PParams p) {
   // frame, each saving its cells like adjust_gamestate would.  Every lane of
   // the session runs 16 / L of the branches, kFanGroup at a time.
   [[maybe_unused]] uint32_t tot_branch = 0;
+  // ---- the per-player form (RB_P2P_FLAG_FANOUT_PER_PLAYER; whole alphabet only): every remote
+  // player is speculated.  B = the oldest first unconfirmed frame over the remote players; each
+  // remote player's own lane presimulates the nb input classes of that player from the cell of B
+  // (confirmed inputs up to its own last added frame, then the class held), each local player's
+  // lane its player once with its confirmed inputs.  A later tick whose rollback starts at B and
+  // in which every remote player's newly confirmed inputs hold one class (or none arrived) then
+  // selects, player by player (try_select).  Columns: branch k of lane l's player (s * L + l) * 16
+  // + k, a local player's chain Spad * L * 16 + s * L + l (planes Spad * L * 17 wide).
+  auto fan_per_player = [&]() __attribute__((always_inline)) {
+    if constexpr (kInFan && !kMtf) {
+      const int lane_base = static_cast<int>(__lane_id()) - lane;
+      int32_t B = INT32_MAX;
+      int nrem = 0;
+#pragma unroll
+      for (int h = 0; h < P; ++h) {
+        const int32_t la = __shfl(q[0].last_added, lane_base + h, 64);
+        if ((p.local_mask >> h) & 1u) continue;
+        B = min(B, (la == kNullFrame ? -1 : la) + 1);
+        ++nrem;
+      }
+      const bool my_remote = lane < P && !((p.local_mask >> lane) & 1u);
+      const int32_t la_own = q[0].last_added;
+      sm_pbase = (la_own == kNullFrame ? -1 : la_own) + 1;
+      const unsigned bslot = static_cast<unsigned>(B >= 0 && B != INT32_MAX ? B % W : 0);
+      const int32_t btag = kLdsC ? lds_tag[bslot * bps + sl] : p.tag[bslot * Spad + s];
+      const bool valid = !(RB_FAN_EXP & 1) && !any_disc && nrem > 0 && B >= 0 && B < cur && B + W > cur && btag == B;
+      constexpr auto AC = AlphabetClasses<G>::value;
+      constexpr int nb = AC.n;
+      uint32_t acp[4];
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) acp[qq] = AC.packed[qq];
+      sm_valid = valid ? (1 | (nb << 8) | (1 << 16)) : 0;
+      sm_base = B;
+      sm_end = cur;
+      sm_player = -1;
+      if (!valid) return;  // session-uniform
+      uint32_t ow[NW];  // this lane's player's words of the cell of B
+      if constexpr (kLdsC) {
+#pragma unroll
+        for (int n = 0; n < NW; ++n) ow[n] = lds_cell[(bslot * NW + n) * bd + tid];
+      } else {
+        load_words<NW>(p.snap + bslot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), ow);
+      }
+      const int h_own = min(lane, P - 1);
+      const bool own_local = (p.local_mask >> h_own) & 1u;
+      const uint32_t pred_own = la_own == kNullFrame ? 0u : ring.get(la_own, h_own, s);
+      uint32_t vin[kFanPre];
+      fan_prefetch(ring, h_own, s, B, cur, own_local, la_own, pred_own, vin);
+      const uint64_t vpk = fan_pack(vin);
+      const unsigned Gs = Spad * static_cast<unsigned>(L) * static_cast<unsigned>(kSpecBranches + 1);
+      const unsigned bcol = (s * static_cast<unsigned>(L) + static_cast<unsigned>(lane)) * kSpecBranches;
+      const unsigned ocol = Spad * static_cast<unsigned>(L) * kSpecBranches + s * L + static_cast<unsigned>(lane);
+      const int nsl = my_remote ? nb : (lane < P ? 1 : 0);  // this lane's chains
+      bool inr = false;
+      if constexpr (G::kHasRangePath && RB_FAN_INRANGE) inr = __all(G::in_range(ow));
+      auto adv = [&](uint32_t (&x)[NW], InRec in) __attribute__((always_inline)) {
+        if constexpr (G::kHasRangePath) {
+          if (inr) {
+            G::template advance<true>(x, in, h_own, 0u, &p.counters[1]);
+            return;
+          }
+        }
+        advance_frame<G>(x, in, h_own, 0u, &p.counters[1]);
+      };
+      auto group = [&](auto ng_tag, int b0) __attribute__((always_inline)) {
+        constexpr int NG = decltype(ng_tag)::value;
+        uint32_t wb[NG][NW];
+        uint32_t rep[NG];
+        bool on[NG];
+        unsigned col[NG];
+#pragma unroll
+        for (int b = 0; b < NG; ++b) {
+          const int k = b0 + b;
+          on[b] = k < nsl;
+          rep[b] = cand_at(acp, k & (kSpecBranches - 1));
+          col[b] = my_remote ? bcol + static_cast<unsigned>(k & (kSpecBranches - 1)) : ocol;
+#pragma unroll
+          for (int n = 0; n < NW; ++n) wb[b][n] = ow[n];
+        }
+        for (int32_t f = B; f < cur; ++f) {
+          if (f > B && !(RB_FAN_EXP & 2)) {  // SaveGameState of frame f in every chain
+            const unsigned slot = static_cast<unsigned>(f % W);
+#pragma unroll
+            for (int b = 0; b < NG; ++b)
+              if (on[b]) store_words<NW>(p.spec_cells + slot * NW * Gs, static_cast<int>(Gs), static_cast<int>(col[b]), wb[b]);
+          }
+          // the player's input of frame f: confirmed up to its last added frame, then the chain's class
+          // (a remote player) or its repeat-last prediction (a local player's inputs are all confirmed)
+          const int j = f - B;
+          uint32_t v;
+          if (j < kFanPre) v = fan_input(vpk, j);
+          else if (own_local || (la_own != kNullFrame && f <= la_own)) v = ring.get(f, h_own, s);
+          else v = pred_own;
+          const bool held = my_remote && !(la_own != kNullFrame && f <= la_own);
+#pragma unroll
+          for (int b = 0; b < NG; ++b)
+            adv(wb[b], static_cast<InRec>(static_cast<uint64_t>(held ? rep[b] : v) << (8 * h_own)));
+        }
+#pragma unroll
+        for (int b = 0; b < NG; ++b)
+          if (on[b]) store_words<NW>(p.spec_state, static_cast<int>(Gs), static_cast<int>(col[b]), wb[b]);
+      };
+      int ns = 0;  // the chain slots the wave runs: the most any of its lanes needs
+#pragma unroll
+      for (int sb = 0; sb < kSpecBranches; ++sb) ns += __any(sb < nsl) ? 1 : 0;
+      for (int b0 = 0; b0 < ns; b0 += kFanGroup) {
+        const int ng = min(kFanGroup, ns - b0);
+        if (ng == 1) group(std::integral_constant<int, 1>{}, b0);
+        else if (ng == 2 || kFanGroup == 2) group(std::integral_constant<int, 2>{}, b0);
+        else if (ng == 3 || kFanGroup == 3) group(std::integral_constant<int, 3>{}, b0);
+        else group(std::integral_constant<int, (kFanGroup >= 4 ? 4 : 3)>{}, b0);
+      }
+      tot_branch += static_cast<uint32_t>(cur - B) * static_cast<uint32_t>(nb * nrem);
+    }
+  };
   auto fan_inlane = [&]() __attribute__((always_inline)) {
+    if constexpr (kInFan && !kMtf) {
+      if (p.spec_per_player) {
+        fan_per_player();
+        return;
+      }
+    }
     if constexpr (kInFan) {
       const int lane_base = static_cast<int>(__lane_id()) - lane;
       int rs = -1;
@@ -2025,9 +2243,13 @@ p2p_kernel(const P2PParams p) {
         p.spec_meta[SM_PLAYER * Spad + s] = sm_player;
         p.spec_meta[SM_VALID * Spad + s] = sm_valid;
 #pragma unroll
-        for (int qq = 0; qq < 4; ++qq) p.spec_meta[(SM_CAND + qq) * Spad + s] = static_cast<int32_t>(sm_cand[qq]);
+        for (int qq = 0; qq < 4; ++qq)
+          if (!p.spec_per_player) p.spec_meta[(SM_CAND + qq) * Spad + s] = static_cast<int32_t>(sm_cand[qq]);
       }
     }
+  }
+  if constexpr (kInFan && !kMtf) {  // per-player fan-out: each lane writes its own player's base row
+    if (in_fan && p.spec_per_player) p.spec_meta[(SM_CAND + lane) * Spad + s] = sm_pbase;
   }
 #if RB_P2P_PHASE
   RB_PH(5);

@@ -28,6 +28,7 @@ struct rb_p2p {
   uint32_t* counters = nullptr;
   unsigned long long* stats = nullptr;  // [ST_COUNT][Spad]
   bool fanout = false;
+  bool per_player = false;   // RB_P2P_FLAG_FANOUT_PER_PLAYER
   bool sync_ticks = false;   // RB_P2P_SYNC_TICKS=1 at create: lock-step ticks (p2p.hpp kAsync off)
   bool fan_generic = false;  // RB_FANOUT_GENERIC=1 at create: fanout_kernel for every game
   uint32_t* spec_state = nullptr;
@@ -256,6 +257,11 @@ rb_status rb_p2p_create(const rb_p2p_config* cfg, rb_p2p** out) {
                  "speculative fan-out needs ex_game with one lane per player or the brawler, no sparse saving");
   if (fanout && (cfg->fanout_candidates < 1 || cfg->fanout_candidates > kSpecBranches))
     return pfail(nullptr, RB_INVALID_REQUEST, "fanout_candidates must be 1..16");
+  const bool per_player = fanout && (cfg->flags & RB_P2P_FLAG_FANOUT_PER_PLAYER) != 0;
+  if (per_player && (!ops->inlane_fanout || ops->input_alphabet > static_cast<uint32_t>(cfg->fanout_candidates)))
+    return pfail(nullptr, RB_INVALID_REQUEST,
+                 "per-player speculation needs independent players (ex_game) and fanout_candidates covering the "
+                 "input alphabet");
   if (static_cast<uint64_t>(cfg->max_prediction) * ops->nw * ops->lanes *
           ((static_cast<uint64_t>(cfg->num_sessions) + 63) / 64 * 64) >= (1ull << 32))
     return pfail(nullptr, RB_INVALID_REQUEST, "batch too large for 32-bit snapshot offsets");
@@ -271,6 +277,7 @@ rb_status rb_p2p_create(const rb_p2p_config* cfg, rb_p2p** out) {
   if (b->block % 64 != 0 || b->block > 256) return pfail(nullptr, RB_INVALID_REQUEST, "block_size must be 64, 128, 192 or 256");
   b->device = cfg->device;
   b->fanout = fanout;
+  b->per_player = per_player;
   if (const char* e = std::getenv("RB_P2P_SYNC_TICKS")) b->sync_ticks = std::atoi(e) != 0;
   if (const char* e = std::getenv("RB_FANOUT_GENERIC")) b->fan_generic = std::atoi(e) != 0;
   rb_p2p* bp = b.get();
@@ -311,7 +318,7 @@ rb_status rb_p2p_create(const rb_p2p_config* cfg, rb_p2p** out) {
   P2P_CREATE(hipMemsetAsync(b->counters, 0, 16, b->stream));
   P2P_CREATE(hipMemsetAsync(b->stats, 0, ST_COUNT * Sp * 8, b->stream));
   if (b->fanout) {
-    const size_t K = kSpecBranches;
+    const size_t K = kSpecBranches + 1;  // (the per-player columns: 16 branches + one own chain per lane)
     P2P_CREATE(hipMalloc(&b->spec_state, K * NW * Gp * 4));
     P2P_CREATE(hipMalloc(&b->spec_cells, W * K * NW * Gp * 4));
     P2P_CREATE(hipMalloc(&b->spec_cs, W * K * Sp * b->ops->cs_bytes));
@@ -435,6 +442,7 @@ P2PParams base_params(const rb_p2p* b) {
   p.fan_generic = b->fan_generic ? 1 : 0;
   p.fan_k = b->cfg.fanout_candidates;
   p.spec_on = b->fanout ? 1 : 0;
+  p.spec_per_player = b->per_player && !b->fan_generic ? 1 : 0;
   p.spec_state = b->spec_state;
   p.spec_cells = b->spec_cells;
   p.spec_cs = b->spec_cs;

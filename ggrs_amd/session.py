@@ -248,7 +248,7 @@ class SessionBuilder:
         return self
 
     def with_speculative_fanout(self, on: bool, candidates: int = 16, adaptive: bool = True,
-                                min_select_permille: int = 0) -> "SessionBuilder":
+                                min_select_permille: int = 0, per_player: bool = False) -> "SessionBuilder":
         """P2P: presimulate `candidates` (1..16) candidate inputs of the
         most-lagging remote handle after every tick (RB_P2P_FLAG_FANOUT,
         BASELINE config 4): the whole input alphabet when it has at most that
@@ -260,6 +260,7 @@ class SessionBuilder:
         self._fanout_k = int(candidates)
         self._fanout_adaptive = bool(adaptive)
         self._fanout_permille = int(min_select_permille)
+        self._fanout_per_player = bool(per_player)  # RB_P2P_FLAG_FANOUT_PER_PLAYER: every remote player
         return self
 
     def with_desync_detection_mode(self, interval: int) -> "SessionBuilder":  # builder.rs:169-172
@@ -306,6 +307,7 @@ class SessionBuilder:
         pc.flags = (self._cfg.flags & L.RB_FLAG_LANE_PER_SESSION) | (
             L.RB_P2P_FLAG_FANOUT if getattr(self, "_fanout", False) else 0) | (
             L.RB_P2P_FLAG_FANOUT_ALWAYS if not getattr(self, "_fanout_adaptive", True) else 0) | (
+            L.RB_P2P_FLAG_FANOUT_PER_PLAYER if getattr(self, "_fanout_per_player", False) else 0) | (
             L.RB_P2P_FLAG_PEER_STATUS if getattr(self, "_peer_status", False) else 0)
         pc.block_size = self._cfg.block_size
         pc.desync_interval = getattr(self, "_desync", 0)

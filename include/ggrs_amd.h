@@ -295,6 +295,17 @@ typedef struct rb_p2p_config {
  * the same either way.  RB_P2P_FLAG_FANOUT_ALWAYS keeps it on. */
 #define RB_P2P_FLAG_FANOUT_ALWAYS 16u
 
+/* Per-player speculation (with RB_P2P_FLAG_FANOUT; games whose players move
+ * independently and whose whole input alphabet fits the candidates: ex_game at
+ * K = 16): every remote player's input classes are presimulated, each in its
+ * own lane, from the oldest first unconfirmed frame B over the remote players,
+ * instead of the one remote player with that oldest frame.  A rollback from B
+ * in which every remote player's newly confirmed inputs hold one class then
+ * becomes a select even when several players mispredicted (the plain fan-out
+ * needs the speculated player to be the only one).  More chains per tick: the
+ * bench reports both forms (bench.py --fanout-mode). */
+#define RB_P2P_FLAG_FANOUT_PER_PLAYER 32u
+
 /* Peers' connect-status reports (update_player_disconnects, p2p_session.rs:707-742):
  * every advance_frame combines what the running endpoints last reported about
  * each player (rb_p2p_receive_peer_connect_status) with the session's own

@@ -194,10 +194,11 @@ def test_oracle_disconnect_resimulates_to_the_disconnected_truth(game, sparse):
 
 
 # ---------------------------------------------------------------------------- device vs oracle
-def gpu_pair(game, S, P, W, d, rd, mask, sparse, lane_per_session=False, fanout=False, candidates=16):
+def gpu_pair(game, S, P, W, d, rd, mask, sparse, lane_per_session=False, fanout=False, candidates=16,
+             per_player=False):
     b = (G.SessionBuilder(game, num_sessions=S).with_num_players(P).with_max_prediction_window(W)
          .with_input_delay(d).with_sparse_saving_mode(sparse).with_remote_input_delay(rd)
-         .with_lane_per_session(lane_per_session).with_speculative_fanout(fanout, candidates))
+         .with_lane_per_session(lane_per_session).with_speculative_fanout(fanout, candidates, per_player=per_player))
     for h in range(P):
         b.add_player(PlayerType.Local if (mask >> h) & 1 else PlayerType.Remote, h)
     sess = b.start_p2p_session()
@@ -474,6 +475,51 @@ def test_gpu_fanout_fused_launches_match_oracle(gpu_available, case):
     assert selects > 0, "no misprediction was served by a branch select"
     assert branch_frames > 0
     assert sess.counters()[2] == 0 and sess.counters()[1] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tpl", [1, 24], ids=["tick", "fused"])
+@pytest.mark.parametrize("case", FANOUT_CASES, ids=[f"P{c[0]}-W{c[1]}-d{c[2]}-rd{c[3]}-m{c[4]}" for c in FANOUT_CASES])
+def test_gpu_per_player_fanout_matches_rollback(gpu_available, case, tpl):
+    # Per-player speculation (RB_P2P_FLAG_FANOUT_PER_PLAYER): every remote player's input classes are
+    # presimulated from the oldest first unconfirmed frame, so rollbacks in which several players
+    # mispredicted become selects too.  One-tick launches (HBM cells) and 24-tick launches (the LDS
+    # snapshot ring): statuses, request counts, cells, states and queues equal the reference's
+    # rollback (the oracle) after every launch, and more rollbacks become selects than with the
+    # one-player fan-out on the same inputs.
+    import torch
+    P, W, d, rd, mask, (lo, hi) = case
+    S, T = 96, 96
+    inputs, upto, rin = synth_network(S, P, T, mask, rd, lo, hi)
+    sess, orc = gpu_pair(G.Game.EX_GAME, S, P, W, d, rd, mask, False, fanout=True, per_player=True)
+    one, _ = gpu_pair(G.Game.EX_GAME, S, P, W, d, rd, mask, False, fanout=True)
+    di, du, dr = (torch.from_numpy(a).cuda() for a in (inputs, upto, rin))
+    for t0 in range(0, T, tpl):
+        t1 = min(T, t0 + tpl)
+        sess.run_ticks(di[t0:t1], du[t0:t1], dr)
+        one.run_ticks(di[t0:t1], du[t0:t1], dr)
+        ost, olf, ona, ons = drive_oracle(orc, mask, inputs, upto, rin, t1, t0=t0)[-1]
+        st, lf, na, ns = sess.status()
+        np.testing.assert_array_equal(st, ost, err_msg=f"status, tick {t1 - 1}")
+        np.testing.assert_array_equal(lf, olf, err_msg=f"rollback frame, tick {t1 - 1}")
+        np.testing.assert_array_equal(na, ona, err_msg=f"AdvanceFrame count, tick {t1 - 1}")
+        np.testing.assert_array_equal(ns, ons, err_msg=f"SaveGameState count, tick {t1 - 1}")
+        if tpl > 1 or t1 % 8 == 0 or t1 == T:
+            compare_state(sess, orc, t1 - 1)
+    adv, saves, loads, selects, branch_frames = sess.totals()
+    assert selects > 0 and branch_frames > 0
+    assert sess.counters()[2] == 0 and sess.counters()[1] == 0
+    if P > 2:  # several remote players: the per-player form selects where the one-player form cannot
+        assert selects > one.totals()[3], (selects, one.totals()[3])
+    assert loads + selects == one.totals()[2] + one.totals()[3]
+
+
+@pytest.mark.gpu
+def test_gpu_per_player_fanout_needs_the_whole_alphabet(gpu_available):
+    with pytest.raises(G.InvalidRequest):  # K = 8 < ex_game's 16 inputs: candidates from a list
+        gpu_pair(G.Game.EX_GAME, 64, 4, 8, 1, 1, 0b0001, False, fanout=True, candidates=8, per_player=True)
+    with pytest.raises(G.InvalidRequest):  # the brawler's players interact
+        gpu_pair(G.Game.BRAWLER, 64, 2, 8, 1, 1, 0b01, False, fanout=True, per_player=True)
 
 
 @pytest.mark.gpu

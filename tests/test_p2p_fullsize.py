@@ -37,10 +37,10 @@ def sample_of(S):
 SAMPLE = sample_of(S_FULL)
 
 
-def batch(P, sparse=False, fanout=False, K=16, S=S_FULL):
+def batch(P, sparse=False, fanout=False, K=16, S=S_FULL, per_player=False):
     b = (G.SessionBuilder(G.Game.EX_GAME, num_sessions=S).with_num_players(P).with_max_prediction_window(W)
          .with_input_delay(D).with_remote_input_delay(RD).with_sparse_saving_mode(sparse)
-         .with_speculative_fanout(fanout, K))
+         .with_speculative_fanout(fanout, K, per_player=per_player))
     for h in range(P):
         b.add_player(PlayerType.Local if h == 0 else PlayerType.Remote, h)
     return b.start_p2p_session()
@@ -165,13 +165,15 @@ def test_gpu_p2p_one_tick_launches_at_full_size(gpu_available):
     assert_same_batch(mid, fused, "8-tick vs fused launches")
 
 
-def test_gpu_c4_fanout_at_full_size(gpu_available):
+@pytest.mark.parametrize("per_player", [False, True], ids=["one-player", "per-player"])
+def test_gpu_c4_fanout_at_full_size(gpu_available, per_player):
     """BASELINE config 4 as the bench runs it (P = 4, K = 16 candidates, the in-kernel fan-out,
-    50-tick launches) at 65,536 sessions: the oracle sample after every launch; the whole batch
-    equals a plain rollback batch on the same inputs, with every rollback a load or a select."""
+    50-tick launches) at 65,536 sessions, speculating the oldest-unconfirmed remote player or every
+    remote player: the oracle sample after every launch; the whole batch equals a plain rollback
+    batch on the same inputs, with every rollback a load or a select."""
     P, T, tpl = 4, 100, 50
     (inputs, upto, rin), (di, du, dr) = network(P, T)
-    spec, plain = batch(P, fanout=True), batch(P)
+    spec, plain = batch(P, fanout=True, per_player=per_player), batch(P)
     smp = Sample(P, inputs, upto, rin)
     for t0 in range(0, T, tpl):
         spec.run_ticks(di[t0:t0 + tpl], du[t0:t0 + tpl], dr)
