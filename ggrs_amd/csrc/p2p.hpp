@@ -607,7 +607,7 @@ constexpr int kLdsCellsMinTicks = RB_LDS_CELLS_MIN_TICKS;
 // Launches of kLdsQMinTicks up to kLdsCellsMinTicks ticks keep the cells in HBM but the input ring
 // in LDS (p2p_kernel kQ; plain path and sparse saving, ex_game's lane-per-player layout).  Measured
 // at 65,536 sessions, us per tick (HBM ring / LDS ring / LDS cells): 2 ticks per launch 7.6 / 8.0 /
-// 12.7, 4: 6.34 / 6.08 / 8.44, 8: 5.57 / 5.02 / 5.97, 16: 5.07 / 4.36 / 4.55 (tools/ab_short.sh).
+// 12.7, 4: 6.34 / 6.08 / 8.44, 8: 5.57 / 5.02 / 5.97, 16: 5.07 / 4.36 / 4.55 (round 4, interleaved A/B, tools/ab.py).
 #ifndef RB_LDSQ_MIN_TICKS
 #define RB_LDSQ_MIN_TICKS 4
 #endif
@@ -705,7 +705,7 @@ constexpr bool inlane_fan() {
   else return false;
 }
 #ifndef RB_FAN_GROUP
-#define RB_FAN_GROUP 4  // A/B (tools/ab_fangroup.sh): 3 measured the same at C4 (206 VGPRs, still 2 waves per
+#define RB_FAN_GROUP 4  // A/B (tools/ab.py, round 4): 3 measured the same at C4 (206 VGPRs, still 2 waves per
 #endif                  // SIMD); 3 with a 3-waves cap (168 VGPRs, 160 B spilled) 8% slower
 constexpr int kFanGroup = RB_FAN_GROUP;  // chains a lane advances together (independent: instruction-level parallelism)
 #ifndef RB_FAN_INRANGE
