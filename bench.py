@@ -525,7 +525,9 @@ def bench_p2p(args):
         bytes_rank = (adv / world * P + saves / world * (state + 6) + loads / world * state
                       + S * args.steps * 8)
         generic_fan = os.environ.get("RB_FANOUT_GENERIC", "0") not in ("", "0")
-        if args.fanout and (generic_fan or brawler):  # fanout_kernel: per branch frame its cell + checksum stored
+        if args.fanout and branch == 0:  # the adaptive fan-out was paused through the timed region: plain ticks
+            pass
+        elif args.fanout and (generic_fan or brawler):  # fanout_kernel: per branch frame its cell + checksum stored
             # and its inputs; per session-tick the base cell load and K branch states stored; per select the
             # selected cells read back
             bytes_rank += branch / world * (state + 2 + P) + S * args.steps * state * (K + 1) + selects / world * state
@@ -546,6 +548,8 @@ def bench_p2p(args):
         roofline = roofline_block(bytes_rank / max(1, launches), avg_kernel_s, args.steps / max(1, launches), launches,
                                   f"p2p_kernel<{gname}>" + ((" + fanout_kernel (per tick)" if generic_fan or brawler
                                                              else " with the in-kernel fan-out (fused P2P ticks)")
+                                                            if args.fanout and branch > 0 else
+                                                            " (the adaptive fan-out paused: plain P2P ticks)"
                                                             if args.fanout
                                                             else (" (one tick per launch)" if tl == 1 else
                                                                   " (fused P2P ticks)")),
