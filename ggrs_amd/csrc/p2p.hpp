@@ -723,7 +723,7 @@ constexpr int kFanGroup = RB_FAN_GROUP;  // chains a lane advances together (ind
 // spills on the plain path)
 // Attribution builds (tools/mkvar.sh -DRB_P2P_EXP=...): 1 drops the game's
 // AdvanceFrame math, 2 its save checksum, 32 returns at entry (the launch
-// floor).  Always 0 in the product.
+// floor), 64 drops the trace rows and work counters.  Always 0 in the product.
 #ifndef RB_P2P_EXP
 #define RB_P2P_EXP 0
 #endif
@@ -2226,18 +2226,23 @@ p2p_kernel(const P2PParams p) {
     p.qs[QS_LAST_CONF * Spad + s] = last_conf;
     p.qs[QS_DISC_FRAME * Spad + s] = disc_frame;
     p.status[s] = status;
-    p.trace[TR_LOAD * Spad + s] = load_frame;
-    p.trace[TR_NADV * Spad + s] = nadv;
-    p.trace[TR_NSAVE * Spad + s] = nsave;
     if (status == kP2PStatusPanic) atomicAdd(&p.counters[2], 1u);
     if (n_thr) atomicAdd(&p.counters[0], n_thr);
-    p.stats[ST_ADV * Spad + s] += tot_adv;
-    p.stats[ST_SAVE * Spad + s] += tot_save;
-    p.stats[ST_LOAD * Spad + s] += tot_load;
-    p.stats[ST_SELECT * Spad + s] += tot_sel;
+    if constexpr (!(RB_P2P_EXP & 64)) {  // (attribution builds: 64 drops the trace and work-counter traffic)
+      p.trace[TR_LOAD * Spad + s] = load_frame;
+      p.trace[TR_NADV * Spad + s] = nadv;
+      p.trace[TR_NSAVE * Spad + s] = nsave;
+      // the work counters by return-less atomics at the L2: a load, add and store here would put one
+      // more memory round trip at the end of every wave (one-tick launches at 1,048,576 sessions, eight
+      // waves per SIMD slot in turn: 140 -> 111 us without the counter traffic, attribution build 64)
+      atomicAdd(&p.stats[ST_ADV * Spad + s], static_cast<unsigned long long>(tot_adv));
+      atomicAdd(&p.stats[ST_SAVE * Spad + s], static_cast<unsigned long long>(tot_save));
+      if (tot_load) atomicAdd(&p.stats[ST_LOAD * Spad + s], static_cast<unsigned long long>(tot_load));
+      if (tot_sel) atomicAdd(&p.stats[ST_SELECT * Spad + s], static_cast<unsigned long long>(tot_sel));
+    }
     if constexpr (kInFan) {
       if (in_fan) {  // the branches' metadata for the next launch's first tick
-        p.stats[ST_BRANCH * Spad + s] += tot_branch;
+        if (tot_branch) atomicAdd(&p.stats[ST_BRANCH * Spad + s], static_cast<unsigned long long>(tot_branch));
         p.spec_meta[SM_BASE * Spad + s] = sm_base;
         p.spec_meta[SM_END * Spad + s] = sm_end;
         p.spec_meta[SM_PLAYER * Spad + s] = sm_player;
