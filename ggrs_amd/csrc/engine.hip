@@ -622,7 +622,9 @@ rb_status rb_run_ticks(rb_batch* b, int32_t n_ticks, const void* inputs, int64_t
     HIP_TRY(b, hipEventSynchronize(b->tick_ev));
     b->tick_pending = false;
   }
-  const bool can_fuse = b->ops->launch_steady_supported(b->cfg.check_distance);
+  const size_t ring_bytes = std::max(static_cast<size_t>(b->W) * b->ops->nw * b->Spad * b->ops->lanes * 4,
+                                     static_cast<size_t>(b->W) * b->Spad * b->ops->cs_bytes);  // cells, checksums
+  const bool can_fuse = b->ops->launch_steady_supported(b->cfg.check_distance, ring_bytes);
   int32_t run_start = -1, run_c0 = 0;
   uint32_t run_tick0 = 0;
   auto flush = [&](int32_t end) -> rb_status {

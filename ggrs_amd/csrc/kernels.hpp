@@ -148,6 +148,57 @@ __device__ __forceinline__ void store_words(uint32_t* __restrict__ base, int Spa
   }
   if constexpr (R & 1) b[s] = w[NW - 1];
 }
+// The same accesses addressed as the array's base (SGPRs) plus a 32-bit per-lane byte offset that
+// carries the slot too (global_* saddr form): per access one scalar multiply for the slot and one
+// 32-bit add per plane group, where the 64-bit form builds a 64-bit address per plane group and
+// slot.  Only for arrays below 4 GiB (the caller checks).  `lane` holds the lane's offset inside a
+// slot for plane group 0 (16 * g bytes: launch constants), `slot_off` the slot's byte offset.
+template <int NW>
+__device__ __forceinline__ void store_words_sa(char* __restrict__ base, uint32_t slot_off, uint32_t Gpad, uint32_t g,
+                                               const uint32_t (&w)[NW]) {
+  constexpr int Q4 = NW / 4, R = NW % 4;
+#pragma unroll
+  for (int j = 0; j < Q4; ++j)
+    *reinterpret_cast<uint4*>(base + (slot_off + j * 16u * Gpad + 16u * g)) =
+        make_uint4(w[4 * j], w[4 * j + 1], w[4 * j + 2], w[4 * j + 3]);
+  uint32_t b = slot_off + Q4 * 16u * Gpad;
+  if constexpr (R >= 2) {
+    *reinterpret_cast<uint2*>(base + (b + 8u * g)) = make_uint2(w[Q4 * 4], w[Q4 * 4 + 1]);
+    b += 8u * Gpad;
+  }
+  if constexpr (R & 1) *reinterpret_cast<uint32_t*>(base + (b + 4u * g)) = w[NW - 1];
+}
+template <int NW>
+__device__ __forceinline__ void load_words_sa(const char* __restrict__ base, uint32_t slot_off, uint32_t Gpad, uint32_t g,
+                                              uint32_t (&w)[NW]) {
+  constexpr int Q4 = NW / 4, R = NW % 4;
+#pragma unroll
+  for (int j = 0; j < Q4; ++j) {
+    const uint4 v = *reinterpret_cast<const uint4*>(base + (slot_off + j * 16u * Gpad + 16u * g));
+    w[4 * j + 0] = v.x;
+    w[4 * j + 1] = v.y;
+    w[4 * j + 2] = v.z;
+    w[4 * j + 3] = v.w;
+  }
+  uint32_t b = slot_off + Q4 * 16u * Gpad;
+  if constexpr (R >= 2) {
+    const uint2 v = *reinterpret_cast<const uint2*>(base + (b + 8u * g));
+    w[Q4 * 4 + 0] = v.x;
+    w[Q4 * 4 + 1] = v.y;
+    b += 8u * Gpad;
+  }
+  if constexpr (R & 1) w[NW - 1] = *reinterpret_cast<const uint32_t*>(base + (b + 4u * g));
+}
+// steady_kernel's cells and checksums in the saddr form, for games whose per-session state is at
+// most 80 B per slot (ex_game: 5 words x up to 4 lanes; the stubs): their whole snapshot ring stays
+// below 4 GiB up to 3.3M sessions at W = 16, and larger batches run per-tick launches
+// (GameOps::launch_steady_supported).  The brawler's 8 KiB cells keep the 64-bit form.  Measured
+// (interleaved A/B, profiles/r05_ab_saddr.log): SyncTest 4.15 -> 4.04 us per tick, the driver's
+// 20-tick call 1.211e11 -> 1.250e11 session-frames/s.
+template <class G>
+constexpr bool steady_saddr() {
+  return G::NWL * G::kLanes * 4 <= 80;
+}
 // host mirror of the plane layout
 inline size_t word_index(int NW, int Spad, int s, int k) {
   const int Q4 = NW / 4, R = NW % 4;
@@ -475,6 +526,7 @@ steady_kernel(const RunParams p) {
   }
   const unsigned Spad = static_cast<unsigned>(p.Spad), Gpad = Spad * L;
   const unsigned slot_words = static_cast<unsigned>(NW) * Gpad;
+  constexpr bool kSA = steady_saddr<G>();  // (the host launches this kernel only for rings below 4 GiB)
 #if RB_WAVE_CLOCK
   const uint64_t wc_start = __builtin_amdgcn_s_memrealtime();
   uint32_t wc_general = 0;  // ticks this wave ran in the general (not in-range) form
@@ -605,8 +657,15 @@ steady_kernel(const RunParams p) {
         ctx.nonce = nonce + static_cast<uint32_t>(k);
         const CS cval = (dbg & 4u) ? CS{} : G::checksum(w, f, lane, ctx);
         const unsigned slot = slot_after(slot0, k);
-        if (!(dbg & 2u)) store_words<NW>(p.snap + slot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), w);
-        csa[slot * Spad + s] = cval;
+        [[maybe_unused]] const uint32_t soff = slot * slot_words * 4u;  // (kSA: the slot's byte offset)
+        if constexpr (kSA) {
+          if (!(dbg & 2u)) store_words_sa<NW>(reinterpret_cast<char*>(p.snap), soff, Gpad, g, w);
+          *reinterpret_cast<CS*>(reinterpret_cast<char*>(csa) + (slot * Spad * static_cast<uint32_t>(sizeof(CS)) +
+                                                                 s * static_cast<uint32_t>(sizeof(CS)))) = cval;
+        } else {
+          if (!(dbg & 2u)) store_words<NW>(p.snap + slot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), w);
+          csa[slot * Spad + s] = cval;
+        }
         if (k == CD) {
           fsa[slot * Spad + s] = cval;  // first save of frame c: first-seen
           recorded = cval;
@@ -617,8 +676,12 @@ steady_kernel(const RunParams p) {
         // AdvanceFrame reaches at frame f is the one this save checksums, so the value is this one
         if constexpr (G::kDisplay) pc = (k == kp) ? cval : pc;
         // Same lane, same address, program order: this load returns the cell just stored.
-        if (k == 1 && more)
-          load_words<NW>(p.snap + slot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), wn);
+        if (k == 1 && more) {
+          if constexpr (kSA)
+            load_words_sa<NW>(reinterpret_cast<const char*>(p.snap), soff, Gpad, g, wn);
+          else
+            load_words<NW>(p.snap + slot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), wn);
+        }
       }
       if (dbg & 1u)
         w[0] += win[k];
@@ -786,7 +849,11 @@ struct GameOps {
   virtual hipError_t launch_steady(const RunParams& p, int cd, int block, hipStream_t st,
                                    const LaunchEv& ev = {}) const = 0;
   static constexpr int kMaxFusedCD = 16;  // steady_kernel instantiations: check distances 1..16
-  bool launch_steady_supported(int cd) const { return cd >= 1 && cd <= kMaxFusedCD; }
+  bool steady_saddr = false;              // steady_saddr<G>(): 32-bit offsets into the snapshot ring
+  // check distances 1..16, and for steady_saddr games a snapshot ring below 4 GiB
+  bool launch_steady_supported(int cd, size_t snap_bytes) const {
+    return cd >= 1 && cd <= kMaxFusedCD && (!steady_saddr || snap_bytes < (size_t{1} << 32));
+  }
   virtual hipError_t launch_report(const void* cs, const int32_t* err, int S, int32_t frame, void* out,
                                    hipStream_t st) const = 0;
   // P2PSession ticks and the speculative fan-out (p2p.hpp); fan-out needs one
@@ -813,6 +880,7 @@ struct GameOpsT final : GameOps {
     fanout_supported = kFanout;
     inlane_fanout = kFanout && inlane_fan<G>();
     input_alphabet = InputAlphabet<G>::value;
+    steady_saddr = rb::steady_saddr<G>();
   }
   void word_loc(int k, int* lane, int* word) const override { G::word_loc(k, lane, word); }
   void init_words(uint32_t* w) const override { G::init(w); }
