@@ -811,6 +811,9 @@ def main():
         # events around every fused launch), so no first-call cost of that path lands inside it
         sess.profile_enable(timing == "launch")
         run(warm_plan)
+        if world > 1:  # one untimed report all-gather: the collective's first-call setup stays out of timing
+            (sess.export_compact_report if compact else sess.export_checksum_report)(sess.current_frame() - 1, reports)
+            (shard.gather_compact if compact else shard.gather_reports)(reports)
         torch.cuda.synchronize()
         sess.profile_take()
         if twin is not None:  # the twin: same warmup, then the timed region's ticks with events
