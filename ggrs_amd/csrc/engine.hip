@@ -106,6 +106,9 @@ struct rb_batch {
   std::unique_ptr<SyncTestPlan> plan;
   int S = 0, Spad = 0, W = 0, P = 0, block = 256;
   bool plan_only = false;
+  // the fused kernel's 32-bit ring offsets (kernels.hpp steady_saddr): rings of at least this many
+  // bytes run per-tick launches.  4 GiB; RB_STEADY_RING_LIMIT lowers it (the fallback's parity test)
+  size_t ring_limit = size_t{1} << 32;
   int device = 0;
   hipStream_t own_stream = nullptr, stream = nullptr;
   // device buffers
@@ -343,6 +346,8 @@ rb_status rb_synctest_create(const rb_config* cfg, rb_batch** out) {
 #if RB_EXPERIMENTS  // steady_pipe_kernel exists in A/B builds only
   if (const char* env = std::getenv("RB_STEADY_PIPE")) b->pipe = std::atoi(env) != 0;
 #endif
+  if (const char* env = std::getenv("RB_STEADY_RING_LIMIT"))
+    b->ring_limit = std::min(b->ring_limit, static_cast<size_t>(std::strtoull(env, nullptr, 10)));
   if (b->block % 64 != 0 || b->block > 256) return fail(nullptr, RB_INVALID_REQUEST, "block_size must be 64, 128, 192 or 256");
   b->plan_only = cfg->device < 0;
   b->device = cfg->device;
@@ -624,7 +629,7 @@ rb_status rb_run_ticks(rb_batch* b, int32_t n_ticks, const void* inputs, int64_t
   }
   const size_t ring_bytes = std::max(static_cast<size_t>(b->W) * b->ops->nw * b->Spad * b->ops->lanes * 4,
                                      static_cast<size_t>(b->W) * b->Spad * b->ops->cs_bytes);  // cells, checksums
-  const bool can_fuse = b->ops->launch_steady_supported(b->cfg.check_distance, ring_bytes);
+  const bool can_fuse = b->ops->launch_steady_supported(b->cfg.check_distance, ring_bytes, b->ring_limit);
   int32_t run_start = -1, run_c0 = 0;
   uint32_t run_tick0 = 0;
   auto flush = [&](int32_t end) -> rb_status {

@@ -21,6 +21,7 @@
 //   frozen[Spad/64] u64       sessions whose advance_frame returns Err (they no longer advance)
 #pragma once
 #include <hip/hip_ext.h>
+#include <algorithm>
 #include <hip/hip_runtime.h>
 
 #include <memory>
@@ -850,9 +851,9 @@ struct GameOps {
                                    const LaunchEv& ev = {}) const = 0;
   static constexpr int kMaxFusedCD = 16;  // steady_kernel instantiations: check distances 1..16
   bool steady_saddr = false;              // steady_saddr<G>(): 32-bit offsets into the snapshot ring
-  // check distances 1..16, and for steady_saddr games a snapshot ring below 4 GiB
-  bool launch_steady_supported(int cd, size_t snap_bytes) const {
-    return cd >= 1 && cd <= kMaxFusedCD && (!steady_saddr || snap_bytes < (size_t{1} << 32));
+  // check distances 1..16, and for steady_saddr games rings below 4 GiB (`limit`)
+  bool launch_steady_supported(int cd, size_t ring_bytes, size_t limit = size_t{1} << 32) const {
+    return cd >= 1 && cd <= kMaxFusedCD && (!steady_saddr || ring_bytes < std::min(limit, size_t{1} << 32));
   }
   virtual hipError_t launch_report(const void* cs, const int32_t* err, int S, int32_t frame, void* out,
                                    hipStream_t st) const = 0;

@@ -482,6 +482,37 @@ def test_run_ticks_fused_parity(gpu_available, game, P, W, cd, d):
     assert t == T
 
 
+def test_run_ticks_ring_limit_falls_back_to_per_tick_launches(gpu_available, monkeypatch):
+    """The fused kernel addresses ex_game's snapshot ring with 32-bit offsets (kernels.hpp
+    steady_saddr), so a batch whose ring reaches 4 GiB runs per-tick launches instead.
+    RB_STEADY_RING_LIMIT lowers that limit: with it the same calls run unfused (the profile
+    covers only every 8th tick) and stay bit-exact with the oracle; without it they fuse."""
+    import torch
+    S, P, W, cd, d, T = 96, 2, 8, 7, 2, 60
+    inputs = synth_inputs(S, P, T, seed=5)
+    dev = torch.from_numpy(inputs).cuda()
+    covered = {}
+    for limit in ("1", None):
+        if limit:
+            monkeypatch.setenv("RB_STEADY_RING_LIMIT", limit)
+        else:
+            monkeypatch.delenv("RB_STEADY_RING_LIMIT", raising=False)
+        sess, orc = make_pair(G.Game.EX_GAME, S, P, W, cd, d)
+        assert sess.run_ticks(dev[:cd + 1]) == cd + 1  # start-up ticks
+        sess.profile_enable(True)
+        assert sess.run_ticks(dev[cd + 1:]) == T - cd - 1
+        covered[limit] = sess.profile_take()[1]
+        for k in range(T):
+            for h in range(P):
+                orc.add_local_input(h, inputs[k, h])
+            orc.advance()
+        compare_cells(sess, orc, P, G.Game.EX_GAME)
+        compare_live(sess, orc, G.Game.EX_GAME)
+        sess.close()
+    assert covered[None] == T - cd - 1  # one fused launch covers every steady tick
+    assert covered["1"] < (T - cd - 1) // 2  # per-tick launches, every 8th one timed
+
+
 def test_run_ticks_fused_mismatch_and_corruption(gpu_available):
     """Mismatches detected inside a fused launch freeze exactly the sessions
     (and report exactly the frames) that per-tick execution reports."""
