@@ -1831,9 +1831,10 @@ p2p_kernel(const P2PParams p) {
 #pragma unroll
           for (int n = 0; n < NW; ++n) wb[b][n] = ow[n];
         }
-        for (int32_t f = B; f < cur; ++f) {
+        unsigned fsl = bslot;  // f % W, kept alongside f (no integer division per frame)
+        for (int32_t f = B; f < cur; ++f, fsl = fsl + 1 == static_cast<unsigned>(W) ? 0u : fsl + 1) {
           if (f > B && !(RB_FAN_EXP & 2)) {  // SaveGameState of frame f in every chain
-            const unsigned slot = static_cast<unsigned>(f % W);
+            const unsigned slot = fsl;
 #pragma unroll
             for (int b = 0; b < NG; ++b)
               if (on[b]) store_words<NW>(p.spec_cells + slot * NW * Gs, static_cast<int>(Gs), static_cast<int>(col[b]), wb[b]);
@@ -1995,9 +1996,10 @@ p2p_kernel(const P2PParams p) {
 #pragma unroll
           for (int n = 0; n < NW; ++n) wb[b][n] = own[b] ? ow[n] : bw[n];
         }
-        for (int32_t f = base; f < cur; ++f) {
+        unsigned fsl = bslot;  // f % W, kept alongside f (no integer division per frame)
+        for (int32_t f = base; f < cur; ++f, fsl = fsl + 1 == static_cast<unsigned>(W) ? 0u : fsl + 1) {
           if (f > base && !(RB_FAN_EXP & 2)) {  // SaveGameState of frame f in every chain
-            const unsigned slot = static_cast<unsigned>(f % W);
+            const unsigned slot = fsl;
 #pragma unroll
             for (int b = 0; b < NG; ++b)
               if (on[b] || own[b])
@@ -2394,7 +2396,8 @@ __global__ void __launch_bounds__(256) fanout_kernel(const FanParams p) {
     ++frames;
   }
   store_words<NW>(p.spec_state, static_cast<int>(Gs), static_cast<int>(g), w);
-  if (k == 0 && lane == 0) p.stats[ST_BRANCH * Spad + s] += static_cast<unsigned long long>(frames) * p.fan_k;
+  if (k == 0 && lane == 0 && frames)
+    atomicAdd(&p.stats[ST_BRANCH * Spad + s], static_cast<unsigned long long>(frames) * p.fan_k);  // (no load round trip)
 }
 
 }  // namespace rb
