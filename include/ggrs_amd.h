@@ -142,7 +142,10 @@ rb_status rb_advance_frame(rb_batch* b);
  * [num_players][num_sessions] Input values (host or device memory).  The host
  * bookkeeping runs tick by tick as in rb_advance_frame; consecutive
  * steady-state ticks (current frame > check_distance, 1 <= check_distance <= 16)
- * execute as ONE fused device launch.  A session whose resimulation
+ * execute as ONE fused device launch (for games of at most 80 B of state per
+ * cell, e.g. ex_game and the stubs, while the batch's snapshot ring is below
+ * 4 GiB: ex_game P=2, W=8 up to 26M sessions; larger rings run one launch per
+ * tick, same results).  A session whose resimulation
  * mismatches stops advancing (as with per-tick calls) while the others run
  * on; with RB_FLAG_CHECKED the call returns RB_MISMATCHED_CHECKSUM if any
  * session has failed by its end.  Bookkeeping errors (RB_INVALID_REQUEST,
