@@ -545,6 +545,31 @@ def test_run_ticks_fused_mismatch_and_corruption(gpu_available):
     compare_cells(sess, orc, P, G.Game.EX_GAME)  # frozen sessions' cells end as after their failing tick
 
 
+def test_random_checksums_fused_mismatch_like_oracle(gpu_available):
+    """The random-checksum stub (tests/stubs.rs RandomChecksumGameStub) through fused
+    launches: its u128 checksums go through the fused kernel's 32-bit-offset checksum
+    stores, and every session fails at the frame per-tick execution reports."""
+    import torch
+    S, P, cd = 70, 2, 2
+    inputs = np.tile(np.arange(30, dtype=np.uint32)[:, None, None], (1, P, S))
+    sess, orc = make_pair(G.Game.STUB_RANDOM_CS, S, P, 8, cd, 2, seed=11)
+    dev = torch.from_numpy(inputs).cuda()
+    with pytest.raises(G.MismatchedChecksum) as ei:
+        sess.run_ticks(dev)
+    first = None
+    for k in range(30):
+        for h in range(P):
+            orc.add_local_input(h, inputs[k, h])
+        kinds, frames = orc.advance()
+        if first is None and (kinds != 0).any():
+            first = np.where(kinds == 3, frames, -1)
+    assert first is not None and (first != -1).all()
+    np.testing.assert_array_equal(ei.value.frames, first)
+    img, _, _ = sess.read_live()
+    oimg, _, _ = orc.read_live()
+    np.testing.assert_array_equal(img, oimg)
+
+
 def test_prepared_ticks_same_as_run_ticks(gpu_available):
     """session.prepare_ticks (bench.py's timed loop: the native call built
     ahead) runs exactly run_ticks: chunks of ticks through prepared calls on
