@@ -664,11 +664,26 @@ __device__ __forceinline__ void q_discard(DevQueue& q, int32_t frame) {
     q.tail = (q.tail == kNullFrame && q.last_added != kQueueLen - 2) ? kNullFrame : frame;
   }
 }
-// input_queue.rs:104-146 input(requested_frame)
-template <class R>
+// input_queue.rs:104-146 input(requested_frame).  kSel: the same decisions as selects around one
+// ring read (the confirmed frame's entry, or the last added one a new prediction repeats; an unused
+// read of a valid slot otherwise), with no divergent branch and so no exec-mask bookkeeping in every
+// AdvanceFrame's input fetch.  Measured (interleaved A/B, profiles/r05_ab_qsel.log): one-tick
+// launches 11.20 -> 10.44 us of wall per tick, 50-tick launches 3.48 -> 3.43 us; with sparse saving
+// 9.70 -> 10.27 us, so the sparse kernels keep the branches.
+template <bool kSel, class R>
 __device__ __forceinline__ uint32_t q_input(DevQueue& q, const R& r, int h, unsigned s, int32_t f) {
   q.last_req = f;
   q.bad |= f < q.tail;  // assert!(requested_frame >= self.inputs[self.tail].frame) (:113)
+  if constexpr (kSel) {
+    const bool np = q.pred_frame < 0;
+    const bool conf = np && f - q.tail < q.len;               // Confirmed (:118-127)
+    const bool blank = f == 0 || q.last_added == kNullFrame;  // blank_input
+    const uint32_t rv = r.get(conf ? f : q.last_added, h, s);
+    const bool newpred = np && !conf;
+    q.pred_val = newpred ? (blank ? 0u : rv) : q.pred_val;
+    q.pred_frame = newpred ? (blank ? 0 : q.last_added + 1) : q.pred_frame;  // (0: NULL_FRAME + 1)
+    return conf ? rv : q.pred_val;
+  }
   if (q.pred_frame < 0) {
     if (f - q.tail < q.len) return r.get(f, h, s);  // Confirmed (:118-127)
     if (f == 0 || q.last_added == kNullFrame) {
@@ -1046,7 +1061,7 @@ p2p_kernel(const P2PParams p) {
       if (q[j].disc && q[j].conn_last < f) {
         dmask |= 1u << h;
       } else {
-        rec |= static_cast<uint64_t>(q_input(q[j], ring, h, s, f)) << (8 * IB * h);
+        rec |= static_cast<uint64_t>(q_input<!kSparse>(q[j], ring, h, s, f)) << (8 * IB * h);
         if constexpr (G::kUsesStatus) dmask |= (q[j].pred_frame >= 0 ? 1u : 0u) << (8 + h);  // InputStatus::Predicted
       }
     }
