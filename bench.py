@@ -169,22 +169,83 @@ def measured_copy_gbps(dev, nbytes=1 << 30, iters=10):
     return gbps
 
 
-def pmc_profile(cfg_key):
-    """The committed rocprofv3 PMC summary of this exact configuration
-    (profiles/*pmc*.json, written by tools/pmc_summary.py; the newest round's
-    file wins), or None.  Its hbm_bytes_per_tick is FETCH_SIZE x2 + WRITE_SIZE
-    per the gfx950 correction in MI355X_MICROARCH.md; its `issue` block holds
-    SQ_INSTS_VALU, the clock and the VALU issue-slot fraction."""
+def source_id():
+    """Identity of the device code a profile describes: a hash of the kernel sources, the
+    header and the build flags (ggrs_amd/csrc/*.hip, *.hpp, Makefile, include/*), the same
+    for every build of the same sources.  A PMC profile is used only for the sources it was
+    taken on."""
     import glob
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(ROOT, "ggrs_amd", "csrc", "*.hip")) +
+                   glob.glob(os.path.join(ROOT, "ggrs_amd", "csrc", "*.hpp")) +
+                   [os.path.join(ROOT, "ggrs_amd", "csrc", "Makefile")] +
+                   glob.glob(os.path.join(ROOT, "include", "*.h*")))
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_profile(cfg_key, fanout_state=None):
+    """The committed rocprofv3 PMC summary of this exact configuration and launch shape
+    (profiles/*pmc*.json, written by tools/pmc_summary.py), taken on the current kernel
+    sources (`source_id`) and, for a fan-out line, with the fan-out in the same state
+    ("active" / "paused") as in the launches timed here; the newest round's file wins.
+    None when there is none: the line is then `unprofiled`.  Its hbm_bytes_per_tick is
+    FETCH_SIZE x2 + WRITE_SIZE (MI355X_MICROARCH.md's gfx950 correction, checked for this
+    engine's access widths by tools/calib_fetch.hip); its `issue` block holds SQ_INSTS_VALU,
+    the clock and the VALU issue-slot fraction."""
+    import glob
+    src = source_id()
     best = None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
         try:
             d = json.load(open(path))
         except Exception:
             continue
-        if d.get("config_key") == cfg_key and d.get("hbm_bytes_per_tick"):
+        if (d.get("config_key") == cfg_key and d.get("hbm_bytes_per_tick") and d.get("source_id") == src
+                and (fanout_state is None or d.get("fanout_state") == fanout_state)):
             best = dict(d, file=os.path.relpath(path, ROOT))
     return best
+
+
+CLOCK_CAL_FILE = os.path.join(ROOT, "profiles", "r06_clock_calibration.json")
+
+
+def dispatch_overhead_us(cfg_key=None):
+    """What rocprofv3's dispatch duration adds to the kernel's own clock (first wave start to
+    last wave end, rb_launch_clock_*): the dispatch's setup before the first wave and its
+    end-of-kernel release after the last, per launch.  Calibrated by running the bench lines
+    under rocprofv3 --kernel-trace and pairing every timed dispatch with its clock span
+    (tools/clock_calib.py -> profiles/r06_clock_calibration.json): the median of this line's
+    configuration when it was profiled, else the median over all lines; (0, None) when absent."""
+    try:
+        d = json.load(open(CLOCK_CAL_FILE))
+        by = d.get("by_config", {})
+        v = by[cfg_key] if cfg_key in by else d["dispatch_overhead_us"]
+        return float(v), os.path.relpath(CLOCK_CAL_FILE, ROOT)
+    except (OSError, KeyError, ValueError):
+        return 0.0, None
+
+
+def kernel_time(spans_us, units, per_unit_dispatches=1, cfg_key=None):
+    """Average kernel time per timed launch (or per tick of a two-kernel tick) from the clock
+    spans: the spans plus the calibrated dispatch overhead of every dispatch.  Returns
+    (seconds per unit, clock-only seconds per unit, overhead us, calibration file)."""
+    ovh, cal = dispatch_overhead_us(cfg_key)
+    clock = sum(spans_us) / max(1, units)
+    return (clock + ovh * per_unit_dispatches) / 1e6, clock / 1e6, ovh, cal
+
+
+def write_meta(**kw):
+    """GGRS_BENCH_META=path (profiled runs, tools/lines.py prof): what the fold needs to key the
+    profile and to pair its dispatches with the clock spans."""
+    path = os.environ.get("GGRS_BENCH_META")
+    if path:
+        with open(path, "w") as f:
+            json.dump(kw, f)
 
 
 STORE_CEILING_FILE = os.path.join(ROOT, "profiles", "r02_calib_write.json")
@@ -199,7 +260,7 @@ def store_ceiling_gbps():
         return None
 
 
-def roofline_block(bytes_per_launch, avg_kernel_s, ticks_per_launch, launches, kernel, prof, model):
+def roofline_block(bytes_per_launch, avg_kernel_s, ticks_per_launch, launches, kernel, prof, model, copy_gbps=None):
     """The bench line's roofline object.  `achieved`/`frac` are the contract's:
     algorithmic bytes per launch (`model` says which bytes) over the measured
     average launch time, against the 8 TB/s spec peak (`frac_basis`).  Next to
@@ -210,18 +271,26 @@ def roofline_block(bytes_per_launch, avg_kernel_s, ticks_per_launch, launches, k
     above 0.7 of the measured store ceiling (what DRAM takes in practice,
     profiles/r02_calib_write.json), "valu" when the VALU issue slots are above 0.7 busy,
     "latency" (dependent chains at low occupancy) otherwise; "unprofiled"
-    when no PMC profile of this configuration is committed."""
+    when no PMC profile of this configuration is committed, or when the profile's traffic
+    over this kernel time would exceed the measured copy ceiling (`copy_gbps`): counters
+    that describe other launches than the ones timed here are refused, not reported."""
     achieved = bytes_per_launch / avg_kernel_s / 1e9
     r = {"bound": "unprofiled", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
          "frac": achieved / HBM_PEAK_GBS, "frac_basis": "algorithmic bytes / kernel time / 8 TB/s HBM spec",
          "traffic": None, "dram_frac": None, "algorithmic_bytes_per_launch": bytes_per_launch, "bytes_model": model,
          "kernel_avg_us": avg_kernel_s * 1e6, "ticks_per_launch": ticks_per_launch, "launches_timed": launches,
          "kernel": kernel}
+    if prof and copy_gbps and prof["hbm_bytes_per_tick"] * ticks_per_launch / avg_kernel_s / 1e9 > copy_gbps:
+        r["pmc_refused"] = (f"{prof['file']}: its traffic over this kernel time would be "
+                            f"{prof['hbm_bytes_per_tick'] * ticks_per_launch / avg_kernel_s / 1e9:.0f} GB/s, above the "
+                            f"measured {copy_gbps:.0f} GB/s copy ceiling")
+        prof = None
     if prof:
         traffic = prof["hbm_bytes_per_tick"] * ticks_per_launch
         r["traffic"] = traffic
         r["dram_frac"] = r["traffic_frac"] = traffic / avg_kernel_s / 1e9 / HBM_PEAK_GBS
         r["pmc_profile"] = prof["file"]
+        r["pmc_source_id"] = prof.get("source_id")
         iss = prof.get("issue")
         if iss:
             r["valu"] = {k: iss[k] for k in ("valu_insts_per_wave", "salu_insts_per_wave", "valu_issue_frac",
@@ -379,11 +448,13 @@ def bench_p2p(args):
     for h in range(P):
         b.add_player(PlayerType.Local if (mask >> h) & 1 else PlayerType.Remote, h)
     stream = torch.cuda.Stream(device=dev)
-    # Timing (as the SyncTest path, GGRS_BENCH_EVENTS): by default the timed region launches without
-    # events and a twin batch, built and fed identically, times the same ticks' launches afterwards.
-    timing = os.environ.get("GGRS_BENCH_EVENTS", "twin")
-    if timing not in ("twin", "launch"):
-        raise SystemExit("GGRS_BENCH_EVENTS: twin or launch")
+    # Timing as the SyncTest path (GGRS_BENCH_EVENTS, GGRS_BENCH_PROFILE): the kernel's own clock on
+    # every timed launch by default; profiled runs warm up one tick per launch, so that the dominant
+    # kernel's every dispatch of the timed shape is a timed one.
+    timing = os.environ.get("GGRS_BENCH_EVENTS", "clock")
+    if timing not in ("clock", "launch"):
+        raise SystemExit("GGRS_BENCH_EVENTS: clock or launch")
+    profiling = os.environ.get("GGRS_BENCH_PROFILE", "0") not in ("", "0")
 
     def new_batch():
         x = b.start_p2p_session()
@@ -391,7 +462,6 @@ def bench_p2p(args):
         return x
 
     sess = new_batch()
-    twin = new_batch() if timing == "twin" else None
     tpl = args.ticks_per_launch
     import ctypes
     lib = G._lib.load()
@@ -422,10 +492,10 @@ def bench_p2p(args):
             torch.cuda.synchronize()
         assert int((rln < 0).sum()) == 0, "a packet did not fit its row"
 
-    def make_run(batch, one_at_a_time=False):
+    def make_run(batch, one_at_a_time=False, tpl=tpl):
         """The timed loop of one batch, every native call's arguments built ahead (a compiled
-        host's loop): only the C calls run inside it.  one_at_a_time (the twin's replay): each
-        call completes before the next is issued, so a launch's own events bracket it alone."""
+        host's loop): only the C calls run inside it.  one_at_a_time: each call completes
+        before the next is issued."""
         settle = torch.cuda.synchronize if one_at_a_time else (lambda: None)
         h_ = batch._h
         if args.wire:  # the remote inputs travel as packets: no delivery tensors on the receiver
@@ -479,18 +549,17 @@ def bench_p2p(args):
         return run
 
     run = make_run(sess)
+    n_timed = len(range(args.warmup, T, tpl)) if not args.wire else args.steps  # launches of the timed region
+    two_kernel = False  # the two-launch fan-out (fanout_kernel between one-tick P2P launches), set below
     with torch.cuda.stream(stream):
         sess.profile_enable(timing == "launch")  # the warmup takes the timed region's path
-        run(0, args.warmup)
+        (make_run(sess, tpl=1) if profiling else run)(0, args.warmup)
         torch.cuda.synchronize()
         sess.profile_take()
-        if twin is not None:
-            twin_run = make_run(twin, one_at_a_time=True)
-            twin.profile_enable(True)
-            twin_run(0, args.warmup)
-            torch.cuda.synchronize()
-            twin.profile_take()
         a0 = sess.totals()
+        if timing == "clock":  # slots for every launch the timed region can make (two per tick at most)
+            sess.launch_clock_arm(2 * args.steps)
+            torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
             torch.cuda.synchronize()
@@ -502,14 +571,7 @@ def bench_p2p(args):
             torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
         kernel_ms, launches = sess.profile_take()
-        if twin is not None:  # the twin's launches of the same ticks, each timed by its own events
-            twin_run(args.warmup, T)
-            torch.cuda.synchronize()
-            kernel_ms, launches = twin.profile_take()
-            same = all((x == y).all() for x, y in zip(twin.read_cells(), sess.read_cells()))
-            twin.close()
-            if not same:
-                raise SystemExit("twin batch diverged from the timed batch")
+        spans = sess.launch_clock_read(2 * args.steps) if timing == "clock" else None
     a1 = sess.totals()
     adv, saves, loads, selects, branch = (a1[i] - a0[i] for i in range(5))
     thr, unexpected, panics = sess.counters()
@@ -541,13 +603,28 @@ def bench_p2p(args):
             # parts; per select the selected branch's parts read back (its frames: about the branch depth)
             ps = state // P
             bytes_rank += branch / world * ps + S * args.steps * K * ps + selects / world * ps * 2
-        avg_kernel_s = kernel_ms / 1e3 / max(1, launches)
+        timer = {"timer": "kernel clock + dispatch overhead" if spans is not None else "HIP events (hipExtLaunchKernel)"}
+        per_tick = False
+        if spans is not None:
+            # one clock slot per kernel launch; the two-launch fan-out (fanout_kernel between one-tick P2P
+            # launches) has two per tick, and its unit is then the tick (both kernels)
+            per_tick = len(spans) > n_timed
+            launches = args.steps if per_tick else len(spans)
+        fan_state = None
+        if args.fanout:  # the state of the adaptive fan-out through the timed launches
+            fan_state = "active" if branch > 0 else "paused"
         cfg_key = (f"p2p {args.game} P={P} W={W} d={args.input_delay} rd={args.remote_delay} lag={lo},{hi} S={S}"
                    + (" sparse" if args.sparse_saving else "") + (f" fanout{'' if K == 16 else K}" if args.fanout else "")
                    + (" per-player" if args.fanout and args.fanout_mode == "per-player" else "")
                    + (" wire" if args.wire else "") + (" wire-replay" if args.wire_replay else ""))
         tl = int(round(args.steps / max(1, launches)))  # the PMC profile of the launch shape timed here
         cfg_key += f" tpl={tl}" if tl != 50 else ""
+        if spans is not None:
+            avg_kernel_s, clock_s, ovh, cal = kernel_time(spans, launches, 2 if per_tick else 1, cfg_key)
+            timer.update({"kernel_clock_us": clock_s * 1e6, "dispatch_overhead_us": ovh, "calibration": cal,
+                          "dispatches": len(spans)})
+        else:
+            avg_kernel_s = kernel_ms / 1e3 / max(1, launches)
         gname = f"Brawler<{P}>" if brawler else f"ExGame<{P},true>"
         roofline = roofline_block(bytes_rank / max(1, launches), avg_kernel_s, args.steps / max(1, launches), launches,
                                   f"p2p_kernel<{gname}>" + ((" + fanout_kernel (per tick)" if generic_fan or brawler
@@ -557,7 +634,12 @@ def bench_p2p(args):
                                                             if args.fanout
                                                             else (" (one tick per launch)" if tl == 1 else
                                                                   " (fused P2P ticks)")),
-                                  pmc_profile(cfg_key), "algorithmic: cells loaded/saved, inputs, deliveries")
+                                  pmc_profile(cfg_key, fan_state), "algorithmic: cells loaded/saved, inputs, deliveries",
+                                  measured_copy_gbps(dev))
+        roofline.update(timer)
+        write_meta(config_key=cfg_key, source_id=source_id(), fanout_state=fan_state, kernel="p2p_kernel",
+                   clock_spans_us=spans, dispatch_overhead_us=timer.get("dispatch_overhead_us"),
+                   kernel_avg_us=avg_kernel_s * 1e6, bytes_per_launch=bytes_rank / max(1, launches))
         line = {
             "metric": "P2P session-frames simulated/sec (node), rollback to the first mispredicted frame",
             "value": adv / elapsed, "unit": "session-frames/s", "n_gpus": world, "steps": args.steps,
@@ -709,15 +791,25 @@ def main():
     # and the warmup has run the fused steady kernel at least once.
     warm = cd + 1 + args.warmup
     RT = args.realtime_ticks  # one-tick-per-call ticks after the timed region (the 60 Hz serving path)
-    # Kernel timing.  An event pair on a launch (hipExtLaunchKernel) costs the host ~7 us per call
-    # and the timed wall ~12 us (tools/sync_probe.py, round 5), so by default the timed region
-    # launches without events ("twin"): a second batch, built and fed identically, runs the very same
-    # ticks with each launch timed by its own events right after the timed region; its sessions'
-    # states are bit-identical, so its launches do the same work.  GGRS_BENCH_EVENTS=launch times
-    # the timed region's own launches instead (rounds 3-4).
-    timing = os.environ.get("GGRS_BENCH_EVENTS", "twin")
-    if timing not in ("twin", "launch"):
-        raise SystemExit("GGRS_BENCH_EVENTS: twin or launch")
+    # Kernel timing (GGRS_BENCH_EVENTS).  "clock" (default): every timed launch records its own first
+    # wave start and last wave end on the chip's 100 MHz constant clock (rb_launch_clock_*; two plain
+    # stores per wave, nothing on the stream or the host inside the timed region), and the kernel time
+    # is that span plus the dispatch overhead rocprofv3 adds to it (dispatch_overhead_us, calibrated
+    # against rocprofv3 --kernel-trace of these lines).  A profiler does not perturb that clock, so a
+    # line run under rocprofv3 reports the kernel time it would without.  "launch": the timed launches'
+    # own HIP events (hipExtLaunchKernel; ~12 us of wall per call, and under rocprofv3 they read 8-40%
+    # high, tools/timer_check.py).
+    timing = os.environ.get("GGRS_BENCH_EVENTS", "clock")
+    if timing not in ("clock", "launch"):
+        raise SystemExit("GGRS_BENCH_EVENTS: clock or launch")
+    # GGRS_BENCH_PROFILE=1 (tools/lines.py prof, the rocprofv3 runs): the warm-up ticks run one
+    # tick_kernel launch each and the live-play block is skipped, so that every dispatch of the
+    # dominant kernel in the profile is a timed launch of the line's shape (its rocprofv3 --stats
+    # average is then the timed launches' average).
+    profiling = os.environ.get("GGRS_BENCH_PROFILE", "0") not in ("", "0")
+    if profiling:
+        RT = 0
+    checked = os.environ.get("GGRS_BENCH_CHECKED", "1") not in ("", "0")
     T = warm + args.steps + RT
     # This rank's shard: global sessions [rank*S, (rank+1)*S); inputs keyed by global id.  With
     # N > 1 the batch also holds A audit replicas: the first A sessions of rank (r+1) % N.
@@ -737,13 +829,12 @@ def main():
     def new_batch():
         b = (G.SessionBuilder(game, num_sessions=S + A, device=local).with_num_players(P)
              .with_max_prediction_window(args.max_prediction).with_check_distance(cd)
-             .with_input_delay(args.input_delay).with_checked_mismatches(False)
+             .with_input_delay(args.input_delay).with_checked_mismatches(checked)
              .with_block_size(args.block_size).start_synctest_session())
         b.set_stream(stream)
         return b
 
     sess = new_batch()
-    twin = new_batch() if timing == "twin" else None  # (the brawler's 4 GiB ring twice: 8 GiB of 288)
     # the desync report: 4 B per session (rb_export_compact_report: 16-bit checksum + mismatch flag and
     # delta; both bench games checksum in 16 bits), or the 24 B rb_checksum_report (GGRS_BENCH_REPORT=full)
     compact = os.environ.get("GGRS_BENCH_REPORT", "compact") == "compact"
@@ -809,26 +900,28 @@ def main():
         return steady_launches
 
     with torch.cuda.stream(stream):
-        warm_plan = chunks(0, warm)
         timed_plan = chunks(warm, warm + args.steps, final_report=True)
-        # the warmup takes the timed region's exact path (with GGRS_BENCH_EVENTS=launch, profiling
-        # events around every fused launch), so no first-call cost of that path lands inside it
-        sess.profile_enable(timing == "launch")
-        run(warm_plan)
+        if profiling:  # every warm-up tick its own tick_kernel launch (see GGRS_BENCH_PROFILE above)
+            for t in range(warm):
+                for h in range(P):
+                    sess.add_local_input(h, dinputs[t, h])
+                sess.advance_frame()
+        else:
+            # the warmup takes the timed region's exact path (with GGRS_BENCH_EVENTS=launch, profiling
+            # events around every fused launch), so no first-call cost of that path lands inside it
+            sess.profile_enable(timing == "launch")
+            run(chunks(0, warm))
         if world > 1:  # one untimed report all-gather: the collective's first-call setup stays out of timing
             (sess.export_compact_report if compact else sess.export_checksum_report)(sess.current_frame() - 1, reports)
             (shard.gather_compact if compact else shard.gather_reports)(reports)
         torch.cuda.synchronize()
         sess.profile_take()
-        if twin is not None:  # the twin: same warmup, then the timed region's ticks with events
-            twin_plan = chunks(warm, warm + args.steps, batch=twin)
-            twin.profile_enable(True)
-            for call, check, _, _ in chunks(0, warm, batch=twin):
-                st = call()
-                if st:
-                    check(st)
+        sess.profile_enable(timing == "launch")
+        fused = 1 <= cd <= 16  # fused steady ticks exist for check distances 1..16 (kernels.hpp kMaxFusedCD)
+        clocked = timing == "clock" and fused
+        if clocked:
+            sess.launch_clock_arm(len(timed_plan))  # (clears the slots on the stream: before the sync below)
             torch.cuda.synchronize()
-            twin.profile_take()
         if world > 1:
             dist.barrier()
             torch.cuda.synchronize()
@@ -855,35 +948,19 @@ def main():
             print(f"[trace] calls {1e6 * (t_call - t0):.1f} us, first sync done at {1e6 * (t_sync - t0):.1f} us, "
                   f"elapsed {1e6 * elapsed:.1f} us, GPU marker to marker {1e3 * ev_a.elapsed_time(ev_b):.1f} us",
                   file=sys.stderr, flush=True)
-        kernel_ms, timed_ticks = sess.profile_take()  # HIP events around every steady_kernel launch
-        if twin is not None:  # the twin's launches of the same ticks, each timed by its own events
-            # One at a time: queued back to back, a launch's start event is taken while the one
-            # before it still runs, and the average read up to 15% above the wall per launch
-            # (SyncTest 50-tick launches: 216 us against 196 us of wall and 187 us in rocprofv3).
-            for call, check, _, _ in twin_plan:
-                st = call()
-                if st:
-                    check(st)
-                torch.cuda.synchronize()
-            kernel_ms, timed_ticks = twin.profile_take()
-            fr = sess.current_frame() - 1  # the newest saved cell of both batches
-            same = twin.current_frame() == fr + 1 and all(
-                (x == y).all() for x, y in zip(twin.read_cell(fr), sess.read_cell(fr)))
-            twin.close()
-            if not same:
-                raise SystemExit("twin batch diverged from the timed batch")
-            sess.profile_enable(True)
+        kernel_ms, timed_ticks = sess.profile_take()  # (GGRS_BENCH_EVENTS=launch, or tick_kernel sampling)
+        spans = sess.launch_clock_read(len(timed_plan)) if clocked else None
+        sess.profile_enable(False)
         gather_ms = [a.elapsed_time(b) for a, b in gather_ev]
         # The 60 Hz serving path, after (outside) the timed region: inputs arrive one tick at a
         # time (ex_game_synctest.rs:50-61), so each tick is its own call and launch.
         rt = None
         if RT:
-            # wall time of RT one-tick calls without profiling events, then the kernel time of each
-            # launch from events over RT more (an event pair per launch adds host time of its own)
+            # wall time of RT/2 one-tick calls, then the kernel time of each launch of RT/2 more from
+            # the kernel's own clock (as the timed region)
             t_rt = warm + args.steps
             half = RT // 2
             rt_calls = [sess.prepare_ticks(dinputs[t_rt + k:t_rt + k + 1])[0] for k in range(RT)]
-            sess.profile_enable(False)
             torch.cuda.synchronize()
             r0 = time.perf_counter()
             for k in range(half):
@@ -891,20 +968,28 @@ def main():
                     raise SystemExit(f"realtime tick {k} failed")
             torch.cuda.synchronize()
             rt_wall = time.perf_counter() - r0
-            sess.profile_enable(True)
-            sess.profile_take()
+            if fused:
+                sess.launch_clock_arm(RT - half)
+            else:
+                sess.profile_enable(True)
             for k in range(half, RT):
                 if rt_calls[k]():
                     raise SystemExit(f"realtime tick {k} failed")
             torch.cuda.synchronize()
-            rt_kernel_ms, rt_ticks = sess.profile_take()
+            if fused:
+                rt_spans = sess.launch_clock_read(RT - half)
+                rt_kernel_s = kernel_time(rt_spans, len(rt_spans), 1, f"{args.game} P={P} cd={cd} W={args.max_prediction} "
+                                          f"d={args.input_delay} S={S} tpl=1")[0]
+            else:
+                rt_kernel_ms, rt_ticks = sess.profile_take()
+                rt_kernel_s = rt_kernel_ms / 1e3 / max(1, rt_ticks)
             rt = {"ticks": RT, "ticks_per_call": 1, "wall_us_per_tick": rt_wall / half * 1e6,
-                  "kernel_us_per_tick": rt_kernel_ms * 1e3 / max(1, rt_ticks),
+                  "kernel_us_per_tick": rt_kernel_s * 1e6,
                   "max_ticks_per_s": half / rt_wall, "headroom_60hz": half / rt_wall / 60.0,
-                  "tick_latency_us": rt_kernel_ms * 1e3 / max(1, rt_ticks),
+                  "tick_latency_us": rt_kernel_s * 1e6,
                   "note": "one tick per rb_run_ticks call (live play, inputs arriving per tick), all sessions of "
-                          "this GPU: wall over the first half (no events), kernel time from HIP events over the "
-                          "second; headroom = sustainable ticks/s / 60"}
+                          "this GPU: wall over the first half, kernel time (the kernel's own clock plus the "
+                          "calibrated dispatch overhead) over the second; headroom = sustainable ticks/s / 60"}
 
     nfail = int((sess.mismatches()[:S] != G.NULL_FRAME).sum())  # owned sessions only
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -922,8 +1007,16 @@ def main():
         value = total / elapsed
         # fused steady ticks exist for check distances 1..16 (kernels.hpp kMaxFusedCD); past that
         # every tick is a tick_kernel launch, timed by events on every 8th one (engine sampling)
-        fused = 1 <= cd <= 16
-        if fused:
+        timer = {"timer": "kernel clock + dispatch overhead" if clocked else "HIP events (hipExtLaunchKernel)"}
+        if clocked:
+            assert len(spans) == launches, (len(spans), launches)
+            ticks_per_launch = args.steps / max(1, launches)
+            tl = int(round(ticks_per_launch))
+            avg_kernel_s, clock_s, ovh, cal = kernel_time(
+                spans, launches, 1, f"{args.game} P={P} cd={cd} W={args.max_prediction} d={args.input_delay} S={S}"
+                + (f" tpl={tl}" if tl != 50 else ""))
+            timer.update({"kernel_clock_us": clock_s * 1e6, "dispatch_overhead_us": ovh, "calibration": cal})
+        elif fused:
             assert timed_ticks == args.steps, (timed_ticks, args.steps)
             avg_kernel_s = kernel_ms / 1e3 / max(1, launches)  # per steady_kernel launch
             ticks_per_launch = timed_ticks / max(1, launches)
@@ -954,15 +1047,20 @@ def main():
         tl = int(round(ticks_per_launch))
         cfg_key = f"{args.game} P={P} cd={cd} W={args.max_prediction} d={args.input_delay} S={S}" + (
             f" tpl={tl}" if tl != 50 else "")
+        copy_gbps = measured_copy_gbps(dev)
         roofline = roofline_block(bytes_per_launch, avg_kernel_s, ticks_per_launch, launches,
                                   ((f"steady_kernel<Brawler<{P}>,{cd}>" if brawler else
                                     f"steady_kernel<ExGame<{P},true>,{cd}>") +
                                    (" (fused steady-state ticks)" if tpl > 1 else " (one tick per launch)"))
                                   if fused else (f"tick_kernel<{'Brawler' if brawler else 'ExGame'}<{P}>> (one launch "
                                                  f"per tick: no fused kernel past check distance 16)"),
-                                  pmc_profile(cfg_key), model)
+                                  pmc_profile(cfg_key), model, copy_gbps)
+        roofline.update(timer)
         roofline["algorithmic_bytes_per_session_tick"] = bpt
-        roofline["measured_copy_GBps"] = measured_copy_gbps(dev)
+        roofline["measured_copy_GBps"] = copy_gbps
+        write_meta(config_key=cfg_key, source_id=source_id(), fanout_state=None, kernel="steady_kernel",
+                   clock_spans_us=spans, dispatch_overhead_us=timer.get("dispatch_overhead_us"),
+                   kernel_avg_us=avg_kernel_s * 1e6, bytes_per_launch=bytes_per_launch)
         if brawler:
             ceil = store_ceiling_gbps()
             roofline["store_ceiling_GBps"] = ceil
@@ -999,6 +1097,7 @@ def main():
                 "max_prediction": args.max_prediction,
                 "check_distance": cd,
                 "input_delay": args.input_delay,
+                "checked_mismatches": checked,
                 "session_frames_per_step_per_session": frames_per_tick,
                 "parallelism": f"session-sharded x{world}" + (f", RCCL allgather of desync reports every "
                                                               f"{args.report_interval} ticks" if world > 1 else ""),

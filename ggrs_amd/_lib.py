@@ -125,6 +125,8 @@ SIGNATURES = [
     ("rb_debug_exgame_inrange", _I32, [_I32, ctypes.c_uint32, ctypes.c_int64, _P]),
     ("rb_profile_enable", _I32, [_P, _I32]),
     ("rb_profile_take", _I32, [_P, ctypes.POINTER(ctypes.c_double), _PI32]),
+    ("rb_launch_clock_arm", _I32, [_P, _I32]),
+    ("rb_launch_clock_read", _I32, [_P, _PU64, _I32, _PI32]),
     ("rb_register_game_plugin", _I32, [ctypes.c_char_p, _PI32]),
     ("rb_p2p_config_init", None, [ctypes.POINTER(RbP2PConfig)]),
     ("rb_p2p_create", _I32, [ctypes.POINTER(RbP2PConfig), ctypes.POINTER(_P)]),
@@ -151,6 +153,8 @@ SIGNATURES = [
     ("rb_p2p_receive_peer_connect_status", _I32, [_P, _I32, _P, _P]),
     ("rb_p2p_profile_enable", _I32, [_P, _I32]),
     ("rb_p2p_profile_take", _I32, [_P, ctypes.POINTER(ctypes.c_double), _PI32]),
+    ("rb_p2p_launch_clock_arm", _I32, [_P, _I32]),
+    ("rb_p2p_launch_clock_read", _I32, [_P, _PU64, _I32, _PI32]),
     ("rb_decode_input_packets", _I32, [_I32, _P, _I32, _I32, _I32, _I32, _I32, _P, ctypes.c_int64, _P, _P, _P, _I32,
                                         _P, _P]),
     ("rb_encode_input_packets", _I32, [_I32, _P, _I32, _I32, _I32, _I32, _P, _I32, _I32, _P, _P, _P, ctypes.c_int64,

@@ -153,6 +153,7 @@ struct rb_batch {
   bool pipe = false;  // fused steady ticks with two ticks in flight (RB_STEADY_PIPE=1 at create; A/B, tests)
   uint32_t simds = 1024;  // SIMDs of the device (MI355X: 256 CUs x 4)
   uint32_t lds_pad = 0;  // RB_LDS_PAD (bytes) at create: dynamic LDS reserved per steady workgroup (A/B)
+  LaunchClock clock;  // rb_launch_clock_arm
 };
 
 namespace {
@@ -186,6 +187,7 @@ rb_status destroy_device(rb_batch* b) {
     (void)hipEventDestroy(pr.first);
     (void)hipEventDestroy(pr.second);
   }
+  b->clock.release();
   if (b->own_stream) (void)hipStreamDestroy(b->own_stream);
   return RB_OK;
 }
@@ -571,6 +573,7 @@ rb_status launch_steady_run(rb_batch* b, const uint8_t* tick_inputs, int64_t str
   r.pipe = b->pipe ? 1 : 0;
   r.lds_pad = b->lds_pad;
   r.many_waves = static_cast<uint64_t>(b->Spad) * b->ops->lanes > 2ull * 64ull * b->simds ? 1u : 0u;
+  r.launch_clock = b->clock.next();
   const bool timed = b->prof;
   LaunchEv ev;  // the kernel's own start / end (hipExtLaunchKernel), no marker packets around it
   if (timed) {
@@ -971,6 +974,19 @@ rb_status rb_profile_enable(rb_batch* b, int32_t on) {
     HIP_TRY(b, hipStreamSynchronize(b->stream));
     b->prof_ticks.resize(b->prof_ev.size());
   }
+  return RB_OK;
+}
+
+rb_status rb_launch_clock_arm(rb_batch* b, int32_t launches) {
+  if (b->plan_only || launches <= 0) return fail(b, RB_INVALID_REQUEST, "rb_launch_clock_arm: plan-only batch or no launches");
+  HIP_TRY(b, hipSetDevice(b->device));
+  HIP_TRY(b, b->clock.arm((static_cast<size_t>(b->Spad) * b->ops->lanes + 63) / 64, static_cast<size_t>(launches), b->stream));
+  return RB_OK;
+}
+
+rb_status rb_launch_clock_read(rb_batch* b, uint64_t* start_end, int32_t cap, int32_t* launches) {
+  if (!b->clock.armed) return fail(b, RB_INVALID_REQUEST, "rb_launch_clock_read: not armed");
+  HIP_TRY(b, b->clock.read(start_end, cap, launches, b->stream));
   return RB_OK;
 }
 

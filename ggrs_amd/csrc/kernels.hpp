@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <memory>
+#include <vector>
 
 #include "../../include/ggrs_amd.h"
 #include "games.hpp"
@@ -443,7 +444,18 @@ struct RunParams {
   int32_t pipe;             // 1: two ticks in flight per lane where the game allows it (steady_pipe.hpp)
   uint32_t lds_pad;         // dynamic LDS bytes per workgroup the launch reserves (unused: caps workgroups per CU)
   uint32_t many_waves;      // the launch puts more than two waves on a SIMD of this device (prio_turn)
+  // rb_launch_clock_arm: when set, every wave stores its start and end on the chip's 100 MHz
+  // constant clock (s_memrealtime) at [2 * wave] and [2 * wave + 1]; the host takes the first
+  // start and the last end (rb_launch_clock_read).  A kernel time taken by the kernel itself: no
+  // host call, event or profiler sits in it.  Plain stores, one lane per wave: no atomics on a
+  // shared address (2,048 waves folding into one word serialise at the memory side: +40 us).
+  unsigned long long* launch_clock;
 };
+
+__device__ __forceinline__ void launch_clock_put(unsigned long long* c, unsigned wave, unsigned which) {
+  const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+  if (__lane_id() == static_cast<unsigned>(__builtin_ctzll(__ballot(1)))) c[2u * wave + which] = t;
+}
 
 // An empty asm that reads v: the compiler must complete the load that
 // produced v before this point (an s_waitcnt counted within the iteration).
@@ -520,6 +532,7 @@ steady_kernel(const RunParams p) {
   const unsigned s = g / L;
   const int lane = static_cast<int>(g % L);
   const bool lead = lane == 0;
+  if (p.launch_clock) launch_clock_put(p.launch_clock, g / 64u, 0u);
   if (s >= static_cast<unsigned>(p.S)) return;
   {
     const unsigned wave0 = __builtin_amdgcn_readfirstlane(s) & ~63u;
@@ -753,6 +766,7 @@ steady_kernel(const RunParams p) {
     }
     if (!more) {
       if (p.live_out_last) store_words<NW>(p.live, static_cast<int>(Gpad), static_cast<int>(g), w);
+      if (p.launch_clock) launch_clock_put(p.launch_clock, g / 64u, 1u);
       break;
     }
     // ---- wait here, inside the iteration, for the loads the next tick uses.
@@ -836,6 +850,59 @@ inline hipError_t rb_launch(K kernel, dim3 grid, dim3 block, uint32_t lds, hipSt
   else hipLaunchKernelGGL(kernel, grid, block, lds, st, args...);
   return hipGetLastError();
 }
+
+// rb_launch_clock_arm / rb_p2p_launch_clock_arm: `cap` launch slots of [waves][start, end] words on
+// the device (launch_clock_put), cleared once when armed, so nothing is added to the launches
+// themselves; every launch of the batch takes the next slot until the slots run out.
+struct LaunchClock {
+  unsigned long long* buf = nullptr;
+  size_t waves = 0, cap = 0, used = 0, alloc = 0;
+  bool armed = false;
+  hipError_t arm(size_t waves_per_launch, size_t launches, hipStream_t st) {
+    const size_t words = 2 * waves_per_launch * launches;
+    if (words > alloc) {
+      if (buf) (void)hipFree(buf);
+      buf = nullptr;
+      alloc = 0;
+      hipError_t e = hipMalloc(&buf, words * sizeof(unsigned long long));
+      if (e != hipSuccess) return e;
+      alloc = words;
+    }
+    waves = waves_per_launch;
+    cap = launches;
+    used = 0;
+    armed = true;
+    return hipMemsetAsync(buf, 0, words * sizeof(unsigned long long), st);
+  }
+  unsigned long long* next() { return armed && used < cap ? buf + 2 * waves * used++ : nullptr; }
+  // per launch slot used: the first wave start and the last wave end (10 ns ticks); disarms
+  hipError_t read(uint64_t* start_end, int32_t out_cap, int32_t* n, hipStream_t st) {
+    std::vector<uint64_t> h(2 * waves * used);
+    hipError_t e = h.empty() ? hipSuccess : hipMemcpyAsync(h.data(), buf, h.size() * 8, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return e;
+    int32_t k = 0;
+    for (size_t l = 0; l < used && k < out_cap; ++l, ++k) {
+      uint64_t lo = ~0ull, hi = 0;
+      for (size_t w = 0; w < waves; ++w) {
+        const uint64_t a = h[2 * (l * waves + w)], z = h[2 * (l * waves + w) + 1];
+        if (a) lo = std::min<uint64_t>(lo, a);
+        hi = std::max<uint64_t>(hi, z);
+      }
+      start_end[2 * k] = lo == ~0ull ? 0 : lo;
+      start_end[2 * k + 1] = hi;
+    }
+    *n = k;
+    armed = false;
+    used = 0;
+    return hipSuccess;
+  }
+  void release() {
+    if (buf) (void)hipFree(buf);
+    buf = nullptr;
+    alloc = 0;
+  }
+};
 
 struct GameOps {
   virtual ~GameOps() = default;

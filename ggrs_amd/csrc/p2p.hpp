@@ -99,9 +99,12 @@ struct InputAlphabet<G, std::void_t<decltype(G::kInputAlphabet)>> {
 // is candidate 0) — the player's queue keeps them as a move-to-front list of
 // its 16 most recent distinct inputs, updated as each input is added (mtf_push),
 // so picking the candidates reads no input history (the list is kept only by
-// launches that speculate, kSpec && kMtf: a batch whose launches do not
-// speculate — peers' connect-status reports on, kernels.hpp launch_p2p — never
-// speculates later, so no stale list is ever read) — then, while the queue has
+// launches that speculate, kSpec && kMtf: while the adaptive fan-out pauses,
+// p2p_engine.hip, or with peers' connect-status reports on, the plain kernels
+// leave it as it was, and the first speculating launch after a pause draws its
+// candidates from that older list — a worse guess, never a wrong result: a
+// select takes a branch only when the confirmed inputs hold its candidate on
+// every frame, try_select) — then, while the queue has
 // seen fewer than K distinct values, the smallest values not yet taken.  Packed
 // 4 per word, unused slots 0xFF.  For the in-kernel fan-out, whose branches are
 // input classes (InputCanon), the list holds classes (DevQueue::mcanon) and the
@@ -353,6 +356,7 @@ struct P2PParams {
   const int32_t* pk_start;
   int32_t* pk_status;  // [P][S] the last tick's decode status per endpoint (wire.hip codes), or null
   int32_t* acks;       // [P][S] after the launch: the newest frame received per endpoint (the ack), or null
+  unsigned long long* launch_clock;  // rb_p2p_launch_clock_arm: this launch's [waves][start, end], or null
 };
 
 // The cells as check_checksum_send_interval sees them.  It runs inside
@@ -809,6 +813,7 @@ p2p_kernel(const P2PParams p) {
   const unsigned s = g / L;
   const int lane = static_cast<int>(g % L);
   const bool lead = lane == 0;
+  if (p.launch_clock) launch_clock_put(p.launch_clock, g / 64u, 0u);
   if (s >= static_cast<unsigned>(p.S)) return;  // whole lane groups leave together
 #if RB_P2P_PHASE
   uint64_t ph[6] = {0, 0, 0, 0, 0, 0};
@@ -1167,7 +1172,7 @@ p2p_kernel(const P2PParams p) {
       if (F > B && ok && has) {  // the branch at F must be the cell the reference loads
         const unsigned fslot = static_cast<unsigned>(F % W);
         uint32_t bw[NW], cw[NW];
-        load_words<NW>(p.spec_cells + fslot * NW * Gs, static_cast<int>(Gs), static_cast<int>(col), bw);
+        load_words<NW>(p.spec_cells + static_cast<size_t>(fslot) * NW * Gs, static_cast<int>(Gs), static_cast<int>(col), bw);
         if constexpr (kLdsC) {
 #pragma unroll
           for (int n = 0; n < NW; ++n) cw[n] = lds_cell[(fslot * NW + n) * bd + tid];
@@ -1186,7 +1191,7 @@ p2p_kernel(const P2PParams p) {
       for (int32_t f = F + 1; f < cur; ++f) {  // the cells adjust would have saved
         const unsigned slot = static_cast<unsigned>(f % W);
         uint32_t cw[NW] = {};
-        if (has) load_words<NW>(p.spec_cells + slot * NW * Gs, static_cast<int>(Gs), static_cast<int>(col), cw);
+        if (has) load_words<NW>(p.spec_cells + static_cast<size_t>(slot) * NW * Gs, static_cast<int>(Gs), static_cast<int>(col), cw);
         if (has) {
           if constexpr (kLdsC) {
 #pragma unroll
@@ -1269,10 +1274,10 @@ p2p_kernel(const P2PParams p) {
         for (int32_t f = base + 1; f < cur; ++f) {  // the cells adjust would have saved
           const unsigned slot = static_cast<unsigned>(f % W);
           uint32_t bw[NW], cw[NW] = {};
-          if (lane == owner) load_words<NW>(p.spec_cells + slot * NW * Gs, static_cast<int>(Gs), static_cast<int>(col), bw);
+          if (lane == owner) load_words<NW>(p.spec_cells + static_cast<size_t>(slot) * NW * Gs, static_cast<int>(Gs), static_cast<int>(col), bw);
 #pragma unroll
           for (int n = 0; n < NW; ++n) bw[n] = static_cast<uint32_t>(__shfl(static_cast<int>(bw[n]), src, 64));
-          if (other) load_words<NW>(p.spec_cells + slot * NW * Gs, static_cast<int>(Gs), static_cast<int>(ocol), cw);
+          if (other) load_words<NW>(p.spec_cells + static_cast<size_t>(slot) * NW * Gs, static_cast<int>(Gs), static_cast<int>(ocol), cw);
           if (lane == rs || other) {
             if (lane == rs) {
 #pragma unroll
@@ -1320,7 +1325,7 @@ p2p_kernel(const P2PParams p) {
       for (int32_t f = base + 1; f < cur; ++f) {  // the cells adjust would have saved
         const unsigned slot = static_cast<unsigned>(f % W);
         uint32_t cw[NW];
-        load_words<NW>(p.spec_cells + slot * NW * Gs, static_cast<int>(Gs), static_cast<int>(col), cw);
+        load_words<NW>(p.spec_cells + static_cast<size_t>(slot) * NW * Gs, static_cast<int>(Gs), static_cast<int>(col), cw);
         store_words<NW>(p.snap + slot * slot_words, static_cast<int>(Gpad), static_cast<int>(g), cw);
         if (lead) {
           csa[slot * Spad + s] = scs[(slot * Spad + s) * kSpecBranches + kk];
@@ -1851,7 +1856,7 @@ p2p_kernel(const P2PParams p) {
             const unsigned slot = fsl;
 #pragma unroll
             for (int b = 0; b < NG; ++b)
-              if (on[b]) store_words<NW>(p.spec_cells + slot * NW * Gs, static_cast<int>(Gs), static_cast<int>(col[b]), wb[b]);
+              if (on[b]) store_words<NW>(p.spec_cells + static_cast<size_t>(slot) * NW * Gs, static_cast<int>(Gs), static_cast<int>(col[b]), wb[b]);
           }
           // the player's input of frame f: confirmed up to its last added frame, then the chain's class
           // (a remote player) or its repeat-last prediction (a local player's inputs are all confirmed)
@@ -2017,7 +2022,7 @@ p2p_kernel(const P2PParams p) {
 #pragma unroll
             for (int b = 0; b < NG; ++b)
               if (on[b] || own[b])
-                store_words<NW>(p.spec_cells + slot * NW * Gs, static_cast<int>(Gs), static_cast<int>(col[b]), wb[b]);
+                store_words<NW>(p.spec_cells + static_cast<size_t>(slot) * NW * Gs, static_cast<int>(Gs), static_cast<int>(col[b]), wb[b]);
           }
           uint32_t v = 0;  // the other player's input of frame f
           if (any_own) {
@@ -2272,6 +2277,7 @@ p2p_kernel(const P2PParams p) {
   if constexpr (kInFan && !kMtf) {  // per-player fan-out: each lane writes its own player's base row
     if (in_fan && p.spec_per_player) p.spec_meta[(SM_CAND + lane) * Spad + s] = sm_pbase;
   }
+  if (p.launch_clock) launch_clock_put(p.launch_clock, g / 64u, 1u);
 #if RB_P2P_PHASE
   RB_PH(5);
   if (p.T == 1 && (g & 63u) == 0 && g / 64 < 4096) {
@@ -2317,6 +2323,7 @@ struct FanParams {
   uint32_t local_mask;
   int32_t fan_generic;  // fanout_kernel even for independent players
   int32_t fan_k;        // candidates (branches) per session, <= kSpecBranches
+  unsigned long long* launch_clock;  // rb_p2p_launch_clock_arm: this launch's [waves][start, end], or null
 };
 
 template <class G>
@@ -2332,6 +2339,7 @@ __global__ void __launch_bounds__(256) fanout_kernel(const FanParams p) {
   const unsigned s = g / LS;
   const int r = static_cast<int>(g % LS);
   const int k = r / L, lane = r % L;  // branch = candidate input, player slot
+  if (p.launch_clock) launch_clock_put(p.launch_clock, g / 64u, 0u);
   if (s >= static_cast<unsigned>(p.S)) return;
   const unsigned Spad = static_cast<unsigned>(p.Spad), Gpad = Spad * L;
   const unsigned Gs = Gpad * kSpecBranches;  // spec plane width: column = this thread's index g
@@ -2373,7 +2381,10 @@ __global__ void __launch_bounds__(256) fanout_kernel(const FanParams p) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) p.spec_meta[(SM_CAND + q) * Spad + s] = static_cast<int32_t>(cand[q]);
   }
-  if (!valid || k >= p.fan_k) return;  // session-uniform (branch-uniform): the whole group leaves
+  if (!valid || k >= p.fan_k) {  // session-uniform (branch-uniform): the whole group leaves
+    if (p.launch_clock) launch_clock_put(p.launch_clock, g / 64u, 1u);
+    return;
+  }
   const uint32_t ck = cand_at(cand, k);
   const unsigned gl = s * L + lane;  // this lane's column in the session-major planes
   uint32_t w[NW];
@@ -2394,7 +2405,7 @@ __global__ void __launch_bounds__(256) fanout_kernel(const FanParams p) {
       CsCtx ctx{0ull, s, 0u};
       const CS c = G::checksum(w, f, lane, ctx);
       const unsigned slot = static_cast<unsigned>(f % W);
-      store_words<NW>(p.spec_cells + slot * NW * Gs, static_cast<int>(Gs), static_cast<int>(g), w);
+      store_words<NW>(p.spec_cells + static_cast<size_t>(slot) * NW * Gs, static_cast<int>(Gs), static_cast<int>(g), w);
       if (lane == 0) cs[(slot * Spad + s) * kSpecBranches + k] = c;
     }
     uint32_t v = 0;
@@ -2412,6 +2423,7 @@ __global__ void __launch_bounds__(256) fanout_kernel(const FanParams p) {
   store_words<NW>(p.spec_state, static_cast<int>(Gs), static_cast<int>(g), w);
   if (k == 0 && lane == 0 && frames)
     atomicAdd(&p.stats[ST_BRANCH * Spad + s], static_cast<unsigned long long>(frames) * p.fan_k);  // (no load round trip)
+  if (p.launch_clock) launch_clock_put(p.launch_clock, g / 64u, 1u);
 }
 
 }  // namespace rb

@@ -42,6 +42,7 @@ struct rb_p2p {
   bool prof = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev;
   size_t prof_used = 0;
+  LaunchClock clock;  // rb_p2p_launch_clock_arm
   // the adaptive fan-out (RB_P2P_FLAG_FANOUT without _ALWAYS, include/ggrs_amd.h)
   struct FanPolicy {
     bool adaptive = false;
@@ -49,6 +50,7 @@ struct rb_p2p {
     bool open = false;           // a measurement window is open (its start sums are in host[0..1])
     bool pending = false;        // its end sums are on their way to host[2..3] (event `ev`)
     int32_t ticks = 0;           // ticks into the window (active) or into the pause (inactive)
+    int32_t since_end = 0;       // ticks since the pending window ended (the decision waits kFanDecideTicks)
     uint32_t min_permille = 150;
     unsigned long long* dev = nullptr;   // [4] device sums: selects, loads (window start; end)
     unsigned long long* host = nullptr;  // [4] pinned copies
@@ -97,6 +99,7 @@ void free_all(rb_p2p* b) {
     (void)hipEventDestroy(pr.first);
     (void)hipEventDestroy(pr.second);
   }
+  b->clock.release();
   if (b->own_stream) (void)hipStreamDestroy(b->own_stream);
 }
 
@@ -265,6 +268,13 @@ rb_status rb_p2p_create(const rb_p2p_config* cfg, rb_p2p** out) {
   if (static_cast<uint64_t>(cfg->max_prediction) * ops->nw * ops->lanes *
           ((static_cast<uint64_t>(cfg->num_sessions) + 63) / 64 * 64) >= (1ull << 32))
     return pfail(nullptr, RB_INVALID_REQUEST, "batch too large for 32-bit snapshot offsets");
+  // the fan-out's branch planes: a slot's offset is 64-bit (p2p.hpp), the words inside one slot
+  // (planes x columns, load_words / store_words) are int offsets: at most 2^31 words per slot (the
+  // brawler at 65,536 sessions is exactly that: 32 planes of 2^26 columns, the last plane's int
+  // offset 31 x 2^26)
+  if (fanout && static_cast<uint64_t>(ops->nw) * ops->lanes * (kSpecBranches + (per_player ? 1 : 0)) *
+                        ((static_cast<uint64_t>(cfg->num_sessions) + 63) / 64 * 64) > (1ull << 31))
+    return pfail(nullptr, RB_INVALID_REQUEST, "batch too large for the fan-out's 31-bit branch-plane offsets");
 
   auto b = std::make_unique<rb_p2p>();
   b->cfg = *cfg;
@@ -318,7 +328,9 @@ rb_status rb_p2p_create(const rb_p2p_config* cfg, rb_p2p** out) {
   P2P_CREATE(hipMemsetAsync(b->counters, 0, 16, b->stream));
   P2P_CREATE(hipMemsetAsync(b->stats, 0, ST_COUNT * Sp * 8, b->stream));
   if (b->fanout) {
-    const size_t K = kSpecBranches + 1;  // (the per-player columns: 16 branches + one own chain per lane)
+    // branch columns per lane column: 16 (fanout_kernel: [session][branch][lane]; the one-player in-kernel
+    // fan-out uses 16 + L of 16 * L), plus one own chain per lane for the per-player form
+    const size_t K = kSpecBranches + (per_player ? 1 : 0);
     P2P_CREATE(hipMalloc(&b->spec_state, K * NW * Gp * 4));
     P2P_CREATE(hipMalloc(&b->spec_cells, W * K * NW * Gp * 4));
     P2P_CREATE(hipMalloc(&b->spec_cs, W * K * Sp * b->ops->cs_bytes));
@@ -457,7 +469,10 @@ namespace {
 // The adaptive fan-out (include/ggrs_amd.h RB_P2P_FLAG_FANOUT_ALWAYS).  Windows of kFanProbeTicks
 // ticks back to back while presimulating; each window's select and LoadGameState sums are reduced on
 // the device into pinned memory at its end (host[2..3], event `ev`) and its start (host[0..1]: the
-// previous window's end).  A call that finds the last measurement landed decides; nothing waits.
+// previous window's end).  The decision is taken kFanDecideTicks ticks after a window's end, at the
+// first call from then on, waiting for the event (long complete by then): so whether a tick
+// speculates depends only on the batch's inputs and call sizes, never on when a copy landed.
+constexpr int32_t kFanDecideTicks = 16;
 rb_status fan_snapshot(rb_p2p* b, int off) {
   P2P_TRY(b, hipMemsetAsync(b->fan.dev + off, 0, 2 * sizeof(unsigned long long), b->stream));
   hipLaunchKernelGGL(fan_sums_kernel, dim3((b->S + 255) / 256), dim3(256), 0, b->stream, b->stats, b->S, b->Spad,
@@ -467,10 +482,19 @@ rb_status fan_snapshot(rb_p2p* b, int off) {
                             hipMemcpyDeviceToHost, b->stream));
   return RB_OK;
 }
+// Branches are valid only for the tick right after the launch that made them (SM_END == current
+// frame); a pause's plain ticks leave the metadata as it was, so it is cleared when presimulation
+// stops and again when it restarts.
+rb_status fan_invalidate(rb_p2p* b) {
+  P2P_TRY(b, hipMemsetAsync(b->spec_meta + static_cast<size_t>(SM_VALID) * b->Spad, 0, static_cast<size_t>(b->Spad) * 4,
+                            b->stream));
+  return RB_OK;
+}
 rb_status fan_before(rb_p2p* b) {
   auto& f = b->fan;
   if (!f.adaptive) return RB_OK;
-  if (f.pending && hipEventQuery(f.ev) == hipSuccess) {
+  if (f.pending && f.since_end >= kFanDecideTicks) {
+    P2P_TRY(b, hipEventSynchronize(f.ev));
     f.pending = false;
     const uint64_t sel = f.host[2] - f.host[0], ld = f.host[3] - f.host[1];
     f.windows += 1;
@@ -481,6 +505,8 @@ rb_status fan_before(rb_p2p* b) {
         f.open = false;
         f.ticks = 0;
         f.turned_off += 1;
+        rb_status r = fan_invalidate(b);
+        if (r != RB_OK) return r;
       }
     }
     if (f.active) {  // the next window started at this one's end
@@ -491,6 +517,8 @@ rb_status fan_before(rb_p2p* b) {
   if (!f.active && f.ticks >= kFanPauseTicks) {  // measure again
     f.active = true;
     f.open = false;
+    rb_status r = fan_invalidate(b);
+    if (r != RB_OK) return r;
   }
   if (f.active && !f.open) {
     rb_status r = fan_snapshot(b, 0);
@@ -504,15 +532,28 @@ rb_status fan_after(rb_p2p* b, int32_t n) {
   auto& f = b->fan;
   if (!f.adaptive) return RB_OK;
   f.ticks += n;
+  if (f.pending) f.since_end += n;
   if (f.active && f.open && !f.pending && f.ticks >= kFanProbeTicks) {
     rb_status r = fan_snapshot(b, 2);
     if (r != RB_OK) return r;
     P2P_TRY(b, hipEventRecord(f.ev, b->stream));
     f.pending = true;
+    f.since_end = 0;
     f.ticks = 0;
   }
   return RB_OK;
 }
+// hipSetDevice for the batch's calls, the caller's current device restored on every return
+struct DeviceScope {
+  int prev = -1;
+  explicit DeviceScope(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceScope() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
 }  // namespace
 
 rb_status rb_p2p_fanout_state(rb_p2p* b, int32_t* active, double* select_fraction, int32_t* windows,
@@ -538,8 +579,8 @@ rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs,
   p.remote_in = static_cast<const uint8_t*>(remote_inputs);
   p.remote_frames = remote_frames;
   p.T = n_ticks;
+  DeviceScope dev_scope(b->device);
   if (b->fanout) {
-    P2P_TRY(b, hipSetDevice(b->device));
     rb_status r = fan_before(b);
     if (r != RB_OK) return r;
   }
@@ -563,7 +604,6 @@ rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs,
   fp.local_mask = b->cfg.local_mask;
   fp.fan_generic = b->fan_generic ? 1 : 0;
   fp.fan_k = b->cfg.fanout_candidates;
-  P2P_TRY(b, hipSetDevice(b->device));
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (b->prof) {
     if (b->prof_used == b->prof_ev.size()) {
@@ -578,6 +618,7 @@ rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs,
   hipError_t e = hipSuccess;
   if (one_launch) {
     // all ticks in one launch (with the in-kernel fan-out); timed by the kernel's own start / end
+    p.launch_clock = b->clock.next();
     e = b->ops->launch_p2p(p, b->block, b->stream, LaunchEv{e0, e1});
   } else {
     if (e0) P2P_TRY(b, hipEventRecord(e0, b->stream));
@@ -588,7 +629,9 @@ rb_status rb_p2p_run_ticks(rb_p2p* b, int32_t n_ticks, const void* local_inputs,
     for (int32_t t = 0; t < n_ticks && e == hipSuccess; ++t) {
       pt.local_in = p.local_in + static_cast<int64_t>(t) * p.local_stride;
       pt.upto = p.upto + static_cast<int64_t>(t) * p.upto_stride;
+      pt.launch_clock = b->clock.next();
       e = b->ops->launch_p2p(pt, b->block, b->stream);
+      fp.launch_clock = b->clock.next();
       if (e == hipSuccess) e = b->ops->launch_fanout(fp, b->block, b->stream);
     }
   }
@@ -625,7 +668,8 @@ rb_status rb_p2p_run_ticks_packets(rb_p2p* b, int32_t n_ticks, const void* local
   p.pk_start = start_frames;
   p.pk_status = decode_status;
   p.acks = acks;
-  P2P_TRY(b, hipSetDevice(b->device));
+  p.launch_clock = b->clock.next();
+  DeviceScope dev_scope(b->device);
   LaunchEv ev;  // the kernel's own start / end (hipExtLaunchKernel)
   if (b->prof) {
     if (b->prof_used == b->prof_ev.size()) {
@@ -848,6 +892,22 @@ rb_status rb_p2p_debug_corrupt(rb_p2p* b, int32_t session, int32_t word, uint32_
     v ^= xor_mask;
     P2P_TRY(b, hipMemcpy(q, &v, 4, hipMemcpyHostToDevice));
   }
+  return RB_OK;
+}
+
+rb_status rb_p2p_launch_clock_arm(rb_p2p* b, int32_t launches) {
+  if (launches <= 0) return pfail(b, RB_INVALID_REQUEST, "rb_p2p_launch_clock_arm: no launches");
+  DeviceScope dev_scope(b->device);
+  // one slot holds the widest launch of the batch: fanout_kernel's 16 branches per session
+  const size_t lanes = static_cast<size_t>(b->Spad) * b->ops->lanes * (b->fanout ? kSpecBranches : 1);
+  P2P_TRY(b, b->clock.arm((lanes + 63) / 64, static_cast<size_t>(launches), b->stream));
+  return RB_OK;
+}
+
+rb_status rb_p2p_launch_clock_read(rb_p2p* b, uint64_t* start_end, int32_t cap, int32_t* launches) {
+  if (!b->clock.armed) return pfail(b, RB_INVALID_REQUEST, "rb_p2p_launch_clock_read: not armed");
+  DeviceScope dev_scope(b->device);
+  P2P_TRY(b, b->clock.read(start_end, cap, launches, b->stream));
   return RB_OK;
 }
 

@@ -303,6 +303,17 @@ class P2PSession(_StreamOrdered):
         self._check(self._lib.rb_p2p_profile_take(self._h, ctypes.byref(ms), ctypes.byref(n)))
         return ms.value, n.value
 
+    def launch_clock_arm(self, launches: int) -> None:
+        """The kernel's own clock for the next ``launches`` launches (rb_p2p_launch_clock_arm)."""
+        self._check(self._lib.rb_p2p_launch_clock_arm(self._h, int(launches)))
+
+    def launch_clock_read(self, cap: int):
+        """Per launch since the arm: microseconds from its first wave's start to its last wave's end."""
+        out = (ctypes.c_uint64 * (2 * cap))()
+        n = ctypes.c_int32()
+        self._check(self._lib.rb_p2p_launch_clock_read(self._h, out, int(cap), ctypes.byref(n)))
+        return [(out[2 * i + 1] - out[2 * i]) / 100.0 for i in range(n.value)]
+
 
 def synth_network(num_sessions: int, num_players: int, ticks: int, local_mask: int, remote_delay: int,
                   min_lag: int = 1, max_lag: int = 4, seed: int = SEED, first_session: int = 0,

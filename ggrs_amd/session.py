@@ -611,6 +611,17 @@ class SyncTestSession(_StreamOrdered):
         _raise(self._lib, self._h, self._lib.rb_profile_take(self._h, ctypes.byref(ms), ctypes.byref(n)))
         return ms.value, n.value
 
+    def launch_clock_arm(self, launches: int) -> None:
+        """The kernel's own clock for the next ``launches`` fused launches (rb_launch_clock_arm)."""
+        _raise(self._lib, self._h, self._lib.rb_launch_clock_arm(self._h, int(launches)))
+
+    def launch_clock_read(self, cap: int):
+        """Per fused launch since the arm: microseconds from its first wave's start to its last wave's end."""
+        out = (ctypes.c_uint64 * (2 * cap))()
+        n = ctypes.c_int32()
+        _raise(self._lib, self._h, self._lib.rb_launch_clock_read(self._h, out, int(cap), ctypes.byref(n)))
+        return [(out[2 * i + 1] - out[2 * i]) / 100.0 for i in range(n.value)]
+
 
 # --------------------------------------------------------------------------- decoding helpers
 def decode_ex_game(images: np.ndarray, num_players: int) -> dict:

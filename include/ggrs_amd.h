@@ -231,6 +231,19 @@ rb_status rb_debug_speed_clamp(int32_t device, const float* vx, const float* vy,
 rb_status rb_profile_enable(rb_batch* b, int32_t on);
 rb_status rb_profile_take(rb_batch* b, double* total_ms, int32_t* launches);
 
+/* The kernel's own clock (measurement only, no reference counterpart: bench.py's
+ * kernel time).  rb_launch_clock_arm(b, n): the next n fused steady launches
+ * (rb_run_ticks) have every wave store its start and end on the chip's 100 MHz
+ * constant clock into a slot of their own (cleared here, once: nothing is added
+ * to the launches' stream).  rb_launch_clock_read(b, out[2 * cap], cap, &n)
+ * waits for the stream, returns per launch the first wave's start and the last
+ * wave's end in 10 ns ticks, and disarms.  No host call or event sits between
+ * the two readings and a profiler does not change them; the dispatch's own
+ * setup and end-of-kernel release fall outside them (bench.py adds the
+ * calibrated difference to rocprofv3's dispatch duration). */
+rb_status rb_launch_clock_arm(rb_batch* b, int32_t launches);
+rb_status rb_launch_clock_read(rb_batch* b, uint64_t* start_end, int32_t cap, int32_t* launches);
+
 /* ===========================================================================
  * P2PSession batches (sessions/p2p_session.rs) — the rollback path.
  *
@@ -465,6 +478,10 @@ rb_status rb_p2p_debug_corrupt(rb_p2p* b, int32_t session, int32_t word, uint32_
 /* HIP event timing of every rb_p2p_run_ticks launch (bench.py): total ms and launches since the last take. */
 rb_status rb_p2p_profile_enable(rb_p2p* b, int32_t on);
 rb_status rb_p2p_profile_take(rb_p2p* b, double* total_ms, int32_t* launches);
+/* rb_launch_clock_arm / _read for P2P batches: every p2p_kernel launch, and
+ * with the two-launch fan-out every fanout_kernel launch, takes a slot. */
+rb_status rb_p2p_launch_clock_arm(rb_p2p* b, int32_t launches);
+rb_status rb_p2p_launch_clock_read(rb_p2p* b, uint64_t* start_end, int32_t cap, int32_t* launches);
 
 /* ===========================================================================
  * Batched input packets (network/compression.rs): one

@@ -76,3 +76,59 @@ def test_gpu_exgame_c4_fanout_stays_on_and_a_high_threshold_pauses_it(gpu_availa
         same(x, plain)
         assert x.totals()[2] + x.totals()[3] == plain.totals()[2]
     assert strict.totals()[4] < always.totals()[4]  # the paused batch presimulated fewer branch frames
+
+
+def test_gpu_fanout_pause_and_resume_equals_plain(gpu_available):
+    """a paused fan-out leaves the branch metadata and the move-to-front lists as they
+    were; presimulation restarts after 960 plain ticks.  The branch rows are invalidated when it
+    stops and when it restarts, so the first ticks after the resume select only branches made
+    after it.  1,200 ticks: a window, a pause, the resumed window and the second pause, each tick
+    equal to a plain rollback batch; branch frames are presimulated again after the resume, and
+    the decisions fall at the same ticks in two identical batches (no race with the measurement)."""
+    import torch
+    P, S, T, tpl = 4, 256, 1200, 25
+    inputs, upto, rin = synth_network(S, P, T, 0b1, RD, 1, 4)
+    di, du, dr = (torch.from_numpy(a).cuda() for a in (inputs, upto, rin))
+    strict = batch(G.Game.EX_GAME, P, S, True, min_select_permille=1000)
+    twin = batch(G.Game.EX_GAME, P, S, True, min_select_permille=1000)
+    plain = batch(G.Game.EX_GAME, P, S, False)
+    branch_at = {}
+    for t0 in range(0, T, tpl):
+        for s in (strict, twin, plain):
+            s.run_ticks(di[t0:t0 + tpl], du[t0:t0 + tpl], dr)  # no synchronisation: decisions must not race
+        if t0 + tpl in (1000, T):
+            branch_at[t0 + tpl] = strict.totals()[4]
+            assert strict.fanout_state() == twin.fanout_state()
+        if t0 % 200 == 0:
+            same(strict, plain)
+    same(strict, plain)
+    same(twin, plain)
+    a, frac, windows, off = strict.fanout_state()
+    assert off >= 2 and windows >= 2, (a, frac, windows, off)
+    assert branch_at[T] > branch_at[1000], branch_at  # presimulated again after the resume
+    assert strict.totals() == twin.totals()
+    assert strict.totals()[2] + strict.totals()[3] == plain.totals()[2]
+    assert strict.totals()[3] > 0
+
+
+def test_gpu_brawler_fanout_branch_slots_above_4g_words(gpu_available):
+    """the brawler's branch cells are [W][32 planes][Spad x 64 lanes x 16 branches]
+    words; at 32,768 sessions one slot is 2^30 words, so a 32-bit slot offset wraps from slot 4 on.
+    The offsets are 64-bit now: with the fan-out always on, a batch of that size equals plain
+    rollback (cells, live states, queues) and selects branches."""
+    import torch
+    P, S, T = 2, 32768, 24
+    inputs, upto, rin = synth_network(S, P, T, 0b1, RD, 1, 4, mask=0xFF)
+    di, du, dr = (torch.from_numpy(a).cuda() for a in (inputs, upto, rin))
+    fan = batch(G.Game.BRAWLER, P, S, True, adaptive=False)
+    plain = batch(G.Game.BRAWLER, P, S, False)
+    for t0 in range(0, T, 4):
+        for s in (fan, plain):
+            s.run_ticks(di[t0:t0 + 4], du[t0:t0 + 4], dr)
+    torch.cuda.synchronize()
+    same(fan, plain)
+    tf, tp = fan.totals(), plain.totals()
+    assert tf[3] > 0, tf  # selects happened, so branch cells of every slot were read back
+    assert tf[2] + tf[3] == tp[2]
+    fan.close()
+    plain.close()

@@ -116,3 +116,18 @@ def test_plan_matches_oracle_errors_for_missing_input_mid_game():
         k, _ = orc.advance()
         assert k[0] == 0
         assert [(int(x.kind), x.frame) for x in r] == orc.trace(0)
+
+
+def test_p2p_create_rejects_fanout_planes_beyond_int_offsets():
+    """a fan-out batch whose branch planes would need more than 2^31 words per
+    snapshot slot is refused at create (no GPU needed: the check runs before any allocation)."""
+    import pytest
+
+    import ggrs_amd as G
+    from ggrs_amd.p2p import PlayerType
+    b = (G.SessionBuilder(G.Game.BRAWLER, num_sessions=65536 + 64).with_num_players(2)
+         .with_speculative_fanout(True, 16))
+    for h in range(2):
+        b.add_player(PlayerType.Local if h == 0 else PlayerType.Remote, h)
+    with pytest.raises(G.InvalidRequest, match="31-bit branch-plane"):
+        b.start_p2p_session()

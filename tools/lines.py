@@ -2,15 +2,18 @@
 
     python3 tools/lines.py bench TAG [NAME ...]   # GPU box: every line, fresh process each, with its CPU
                                                   # baseline -> gpurun_out/bench_TAG_NAME.jsonl
-    python3 tools/lines.py prof TAG [NAME ...]    # GPU box: rocprofv3 --kernel-trace --stats and four
-                                                  # --pmc passes per line -> gpurun_out/prof_TAG_NAME/
+    python3 tools/lines.py prof TAG [NAME ...]    # GPU box: the line's own command under rocprofv3
+                                                  # --kernel-trace --stats and four --pmc passes
+                                                  # (GGRS_BENCH_PROFILE=1) -> gpurun_out/prof_TAG_NAME/
     python3 tools/lines.py fold TAG [NAME ...]    # here: profiles/TAG_NAME_{kernel_stats.csv,pmc.json}
                                                   # (tools/pmc_summary.py), keyed like bench.py's lookup
     python3 tools/lines.py copy TAG [NAME ...]    # here: gpurun_out/bench_TAG_* -> profiles/
 
-Each line: the bench.py arguments of the bench run, the arguments of the profiled run (same
-configuration and launch shape, fewer steps, no CPU baseline), bench.py's profile key for it and
-the ticks per timed launch.  The PMC passes follow MI355X_MICROARCH.md's slot budget: FETCH_SIZE
+Each line: the bench.py arguments of the bench run, (unused since round 6: the profiled run is
+the bench run's own command), bench.py's profile key for it and the ticks per timed launch.
+The profiled runs set GGRS_BENCH_PROFILE=1: warm-up ticks one launch each and no live-play
+block, so that the dominant kernel's every dispatch in the --stats summary is a timed launch of
+the line (its AverageNs is the timed launches' average, the line's frac recomputes from it).  The PMC passes follow MI355X_MICROARCH.md's slot budget: FETCH_SIZE
 alone, WRITE_SIZE alone, 8 SQ counters + GRBM, the L2 hit/miss pair; each under its own KILL
 timeout (a pass that over-asks for counters hangs instead of failing).
 """
@@ -95,6 +98,8 @@ def run(cmd, log, timeout):
 
 def bench(tag, names):
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    for k in ("GGRS_BENCH_PROFILE", "GGRS_BENCH_META"):
+        os.environ.pop(k, None)
     for n in names:
         out = os.path.join(ROOT, "gpurun_out", f"bench_{tag}_{n}")
         rc = run(["python3", "-u", "bench.py"] + LINES[n][0].split(), out + ".log", 900)
@@ -117,12 +122,13 @@ def prof(tag, names):
     for n in names:
         d = os.path.join(ROOT, "gpurun_out", f"prof_{tag}_{n}")
         os.makedirs(d, exist_ok=True)
-        # the profiled runs time their own launches (GGRS_BENCH_EVENTS=launch, no twin batch), and each
-        # warmup is one launch of the timed shape, so every dominant-kernel dispatch has the same ticks
-        os.environ["GGRS_BENCH_EVENTS"] = "launch"
-        base = ["python3", "-u", "bench.py"] + LINES[n][1].split() + ["--no-cpu-baseline", "--realtime-ticks", "0"]
+        # the line's own command, timed by the kernel's clock (which rocprofv3 does not perturb), its
+        # warm-up one launch per tick (GGRS_BENCH_PROFILE=1)
+        os.environ["GGRS_BENCH_PROFILE"] = "1"
+        base = ["python3", "-u", "bench.py"] + LINES[n][0].split() + ["--no-cpu-baseline"]
         passes = [("stats", ["--kernel-trace", "--stats"])] + [(k, ["--pmc"] + v.split()) for k, v in PMC.items()]
         for sub, args in passes:
+            os.environ["GGRS_BENCH_META"] = os.path.join(d, f"{sub}_meta.json")
             cmd = ["rocprofv3"] + args + ["-d", os.path.join(d, sub), "-o", "run", "--output-format", "csv", "--"] + base
             if run(cmd, os.path.join(d, sub + ".log"), 300) != 0:
                 return 1

@@ -2,6 +2,13 @@
 
 usage: python3 tools/pmc_summary.py <gpurun_out/prof_TAG> <TAG> [config_key] [ticks_per_launch]
 
+The profiled runs (tools/lines.py prof) run the bench line's own command with
+GGRS_BENCH_PROFILE=1 and write <pass>_meta.json (bench.py write_meta): the profile key,
+the kernel-source id and fan-out state the launches ran with, and the kernel's own clock
+span of every timed launch.  Those keys override the arguments, and every timed dispatch
+of the kernel trace is paired with its clock span ("clock_vs_rocprof": rocprofv3's
+duration minus the clock span, the dispatch overhead bench.py adds).
+
 Writes profiles/<TAG>_kernel_stats.csv (rocprofv3 --stats, verbatim) and
 profiles/<TAG>_pmc.json: per-kernel average counters per launch, and for the
 dominant kernel (steady_kernel, or p2p_kernel for a P2P bench) the HBM bytes per launch and per tick:
@@ -54,6 +61,14 @@ def main():
     os.makedirs(prof, exist_ok=True)
     stats = find(os.path.join(d, "stats"), "*kernel_stats.csv")
     summary = {"tag": tag, "config_key": cfg_key, "ticks_per_launch": tpl, "kernels": {}}
+    meta_path = os.path.join(d, "stats_meta.json")
+    meta = json.load(open(meta_path)) if os.path.exists(meta_path) else {}
+    if meta:
+        summary["config_key"] = meta["config_key"]
+        summary["source_id"] = meta.get("source_id")
+        summary["fanout_state"] = meta.get("fanout_state")
+        summary["line_kernel_avg_us"] = meta.get("kernel_avg_us")
+        summary["bytes_per_launch"] = meta.get("bytes_per_launch")
     if stats:
         shutil.copy(stats[0], os.path.join(prof, f"{tag}_kernel_stats.csv"))
         with open(stats[0]) as f:
@@ -116,6 +131,26 @@ def main():
                 "l2_hit": (e["TCC_HIT_sum"] / (e["TCC_HIT_sum"] + e["TCC_MISS_sum"]))
                 if e.get("TCC_HIT_sum") is not None and e.get("TCC_MISS_sum") is not None else None,
             }
+    # the timed dispatches' rocprofv3 durations against the kernel's own clock spans (same run)
+    spans = meta.get("clock_spans_us")
+    traces = find(os.path.join(d, "stats"), "*kernel_trace.csv")
+    if spans and traces and summary.get("dominant_kernel"):
+        with open(traces[0]) as f:
+            rows = [r for r in csv.DictReader(f) if ("p2p_kernel" in r["Kernel_Name"] or "steady_kernel" in r["Kernel_Name"]
+                                                     or "fanout_kernel" in r["Kernel_Name"])]
+        rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+        dom = summary["dominant_kernel"]
+        # timed launches = the trace's last len(spans) dispatches of the kernel(s) the clock covers
+        # (with GGRS_BENCH_PROFILE=1 the warm-up ran other kernels; the two-launch fan-out
+        # alternates p2p_kernel and fanout_kernel)
+        cand = [r for r in rows if short(r["Kernel_Name"]) == dom or "fanout_kernel" in r["Kernel_Name"]]
+        if len(cand) >= len(spans):
+            cand = cand[-len(spans):]
+            dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in cand]
+            diff = sorted(a - b for a, b in zip(dur, spans))
+            summary["clock_vs_rocprof"] = {
+                "dispatches": len(dur), "rocprof_avg_us": sum(dur) / len(dur), "clock_avg_us": sum(spans) / len(spans),
+                "overhead_median_us": diff[len(diff) // 2], "overhead_min_us": diff[0], "overhead_max_us": diff[-1]}
     out = os.path.join(prof, f"{tag}_pmc.json")
     with open(out, "w") as f:
         json.dump(summary, f, indent=1, sort_keys=True)
