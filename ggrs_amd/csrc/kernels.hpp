@@ -100,6 +100,7 @@ struct KParams {
   int32_t* live_frame;
   unsigned long long* frozen;
   uint32_t* counters;  // [0] sessions failed, [1] unexpected-path count
+  uint32_t* fail_flag;  // host-mapped word set to 1 when a session fails (checked mode), or null
   const void* in_ptr[4];
   int32_t in_mode;  // 0: no new input, 1: one array per player, 2: packed [S][P]
   int32_t S, Spad, W;
@@ -397,6 +398,7 @@ __global__ void __launch_bounds__(256) tick_kernel(const KParams p) {
     p.live_frame[s] = p.f0 + p.n_steps;  // the session stops at the end of this tick
     atomicOr(&p.frozen[s >> 6], 1ull << (s & 63));
     atomicAdd(&p.counters[0], 1u);
+    if (p.fail_flag) *p.fail_flag = 1u;  // (every failing lead lane stores the same word)
   }
 }
 
@@ -433,6 +435,7 @@ struct RunParams {
   int32_t* live_frame;
   unsigned long long* frozen;
   uint32_t* counters;
+  uint32_t* fail_flag;     // host-mapped word set to 1 when a session fails (checked mode), or null
   const uint8_t* in_base;  // tick t, player q: in_base + t*in_stride + q*S*kInputBytes
   int64_t in_stride;
   int32_t S, Spad, W, delay;
@@ -761,6 +764,7 @@ steady_kernel(const RunParams p) {
         p.live_frame[s] = c + 1;
         atomicOr(&p.frozen[s >> 6], 1ull << (s & 63));
         atomicAdd(&p.counters[0], 1u);
+        if (p.fail_flag) *p.fail_flag = 1u;
       }
       return;  // advance_frame returns Err for this session from the next tick on
     }
