@@ -448,13 +448,14 @@ def bench_p2p(args):
     for h in range(P):
         b.add_player(PlayerType.Local if (mask >> h) & 1 else PlayerType.Remote, h)
     stream = torch.cuda.Stream(device=dev)
-    # Timing as the SyncTest path (GGRS_BENCH_EVENTS, GGRS_BENCH_PROFILE): the kernel's own clock on
-    # every timed launch by default; profiled runs warm up one tick per launch, so that the dominant
-    # kernel's every dispatch of the timed shape is a timed one.
+    # Timing as the SyncTest path (GGRS_BENCH_EVENTS): the kernel's own clock on every timed launch by
+    # default.  The warm-up runs in the timed region's call sizes whether or not the run is profiled:
+    # the adaptive fan-out decides by ticks and calls, so a profiled run must take the same decisions
+    # (tools/lines.py picks warm-ups that are whole timed launches, so every dispatch of the dominant
+    # kernel has the timed shape).
     timing = os.environ.get("GGRS_BENCH_EVENTS", "clock")
     if timing not in ("clock", "launch"):
         raise SystemExit("GGRS_BENCH_EVENTS: clock or launch")
-    profiling = os.environ.get("GGRS_BENCH_PROFILE", "0") not in ("", "0")
 
     def new_batch():
         x = b.start_p2p_session()
@@ -492,7 +493,7 @@ def bench_p2p(args):
             torch.cuda.synchronize()
         assert int((rln < 0).sum()) == 0, "a packet did not fit its row"
 
-    def make_run(batch, one_at_a_time=False, tpl=tpl):
+    def make_run(batch, one_at_a_time=False):
         """The timed loop of one batch, every native call's arguments built ahead (a compiled
         host's loop): only the C calls run inside it.  one_at_a_time: each call completes
         before the next is issued."""
@@ -553,7 +554,7 @@ def bench_p2p(args):
     two_kernel = False  # the two-launch fan-out (fanout_kernel between one-tick P2P launches), set below
     with torch.cuda.stream(stream):
         sess.profile_enable(timing == "launch")  # the warmup takes the timed region's path
-        (make_run(sess, tpl=1) if profiling else run)(0, args.warmup)
+        run(0, args.warmup)
         torch.cuda.synchronize()
         sess.profile_take()
         a0 = sess.totals()

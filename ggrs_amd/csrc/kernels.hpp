@@ -1023,7 +1023,7 @@ struct GameOpsT final : GameOps {
       // only the input ring in LDS (kQ below): the LDS cells (79 KiB per 256 threads) fit two
       // workgroups per CU, kQ four (131,072 sessions, lag 1-4: 6.72 -> 5.25 us per tick; at 65,536
       // sessions, two waves per SIMD, the LDS cells stay faster, 3.43 against 3.81)
-      constexpr bool kHasQ = !kSpec && !kNet && G::kLanes > 1;
+      constexpr bool kHasQ = (!kSpec || (RB_SPEC_Q && inlane_fan<G>())) && !kNet && G::kLanes > 1;
       if (p2p_lds_cells<G>(p.W, block) && p.T >= kLdsCellsMinTicks && (!kSpec || !p.fan_generic) &&
           !(kHasQ && p.many_waves)) {
         // lane-asynchronous ticks (plain path and sparse saving) unless the batch asked for lock-step
@@ -1037,8 +1037,8 @@ struct GameOpsT final : GameOps {
         return rb_launch(k, dim3(grid), dim3(block), static_cast<uint32_t>(lds), st, ev, p);
       }
     }
-    if constexpr (!kSpec && !kNet && p2p_lds_queue<G>() && G::kLanes > 1) {
-      if (p.T >= kLdsQMinTicks) {  // the input ring alone in LDS (kLdsQMinTicks)
+    if constexpr ((!kSpec || (RB_SPEC_Q && inlane_fan<G>())) && !kNet && p2p_lds_queue<G>() && G::kLanes > 1) {
+      if (p.T >= kLdsQMinTicks && (!kSpec || (p.many_waves && !p.fan_generic))) {  // the input ring alone in LDS
         auto k = p2p_kernel<G, kSpec, kSparse, kNet, false, false, false, kMtf, true>;
         lds = p2p_lds_bytes<G, true>(block);
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,

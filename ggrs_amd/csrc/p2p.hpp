@@ -315,8 +315,8 @@ struct P2PParams {
   int32_t* status;          // [Spad] rb_status of the session's last advance_frame
   int32_t* trace;           // [TR_COUNT][Spad]
   uint32_t* counters;       // [0] threshold hits, [1] unexpected-path count, [2] panics
-  // per-session work counters [ST_COUNT][Spad] (no same-address atomics: each
-  // session's lead lane owns its column; the host sums on demand)
+  // work counters [ST_COUNT][Spad]: a wave's sum at its first session's column (or per session,
+  // see the end of p2p_kernel); only their sums are read
   unsigned long long* stats;
   // speculative fan-out (spec_on = 0: plain P2P).  fanout_kernel (below, a
   // launch of its own between one-tick P2P launches): branch-major columns
@@ -764,6 +764,15 @@ constexpr int kFanGroup = RB_FAN_GROUP;  // chains a lane advances together (ind
 #ifndef RB_P2P_WAVES_PER_EU
 #define RB_P2P_WAVES_PER_EU 1  // >1: ask the compiler for that many waves per SIMD (VGPR cap; A/B builds)
 #endif
+// RB_SPEC_Q: the in-kernel fan-out of a batch with more than two waves per SIMD keeps its cells in HBM
+// and only the input ring in LDS (kQ), capped at RB_SPEC_Q_WAVES waves per SIMD, instead of the LDS
+// snapshot ring's two workgroups per CU
+#ifndef RB_SPEC_Q
+#define RB_SPEC_Q 0
+#endif
+#ifndef RB_SPEC_Q_WAVES
+#define RB_SPEC_Q_WAVES 3
+#endif
 // kMtf (fan-out batches only): the candidates come from the queues' move-to-front lists, for an
 // alphabet larger than K; otherwise (ex_game at K = 16) they are the alphabet itself, and the lists
 // are neither kept nor read (no registers held for them).
@@ -798,7 +807,7 @@ template <class G, bool kSpec, bool kSparse, bool kNet, bool kLdsC, bool kAsync,
 // The launches that keep the cells in HBM on the plain / sparse path (kQ, and the one-tick launches
 // of live play) are capped at 128 VGPRs the same way: four waves per SIMD once a batch has them.
 __global__ void __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu((kQ || (!kLdsC && !kSpec && !kNet)) ? 4 : RB_P2P_WAVES_PER_EU)))
+__attribute__((amdgpu_waves_per_eu((kQ && kSpec) ? RB_SPEC_Q_WAVES : (kQ || (!kLdsC && !kSpec && !kNet)) ? 4 : RB_P2P_WAVES_PER_EU)))
 p2p_kernel(const P2PParams p) {
   static_assert(!kAsync || (kLdsC && !kSpec && !kNet), "lane-asynchronous ticks: plain or sparse path, LDS cells");
   static_assert(!kWire || (!kSpec && !kSparse && !kNet && !kAsync), "packet-fed ticks: the plain lock-step path");
@@ -2241,6 +2250,32 @@ p2p_kernel(const P2PParams p) {
       }
     }
   }
+  // The work counters by return-less atomics at the L2 (a load, add and store would put one more
+  // memory round trip at the end of every wave: one-tick launches at 1,048,576 sessions, eight waves
+  // per SIMD slot in turn, 140 -> 111 us without the counter traffic, attribution build 64).  Only
+  // their sums are ever read (rb_p2p_totals, the adaptive fan-out's measurement), so a wave whose
+  // lanes are all here adds its sessions' counts up first (cross-lane sums) and its first lane adds
+  // them to the wave's first session's column: one atomic per counter and wave instead of one per
+  // counter and session.  A wave with lanes gone (a panicked session, the padding past S) adds per
+  // session as before.
+  [[maybe_unused]] bool wave_summed = false;
+  if constexpr (!(RB_P2P_EXP & 64)) {
+    if (__ballot(1) == ~0ull) {
+      uint32_t c[4] = {lead ? tot_adv : 0u, lead ? tot_save : 0u, lead ? tot_load : 0u, lead ? tot_sel : 0u};
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) c[i] += static_cast<uint32_t>(__shfl_xor(static_cast<int>(c[i]), o, 64));
+      if ((g & 63u) == 0) {
+        const unsigned s0 = s;  // the wave's first session
+        atomicAdd(&p.stats[ST_ADV * Spad + s0], static_cast<unsigned long long>(c[0]));
+        atomicAdd(&p.stats[ST_SAVE * Spad + s0], static_cast<unsigned long long>(c[1]));
+        if (c[2]) atomicAdd(&p.stats[ST_LOAD * Spad + s0], static_cast<unsigned long long>(c[2]));
+        if (c[3]) atomicAdd(&p.stats[ST_SELECT * Spad + s0], static_cast<unsigned long long>(c[3]));
+      }
+      wave_summed = true;
+    }
+  }
   if (lead) {
     p.qs[QS_CUR * Spad + s] = cur;
     p.qs[QS_LAST_SAVED * Spad + s] = last_saved;
@@ -2253,13 +2288,12 @@ p2p_kernel(const P2PParams p) {
       p.trace[TR_LOAD * Spad + s] = load_frame;
       p.trace[TR_NADV * Spad + s] = nadv;
       p.trace[TR_NSAVE * Spad + s] = nsave;
-      // the work counters by return-less atomics at the L2: a load, add and store here would put one
-      // more memory round trip at the end of every wave (one-tick launches at 1,048,576 sessions, eight
-      // waves per SIMD slot in turn: 140 -> 111 us without the counter traffic, attribution build 64)
-      atomicAdd(&p.stats[ST_ADV * Spad + s], static_cast<unsigned long long>(tot_adv));
-      atomicAdd(&p.stats[ST_SAVE * Spad + s], static_cast<unsigned long long>(tot_save));
-      if (tot_load) atomicAdd(&p.stats[ST_LOAD * Spad + s], static_cast<unsigned long long>(tot_load));
-      if (tot_sel) atomicAdd(&p.stats[ST_SELECT * Spad + s], static_cast<unsigned long long>(tot_sel));
+      if (!wave_summed) {
+        atomicAdd(&p.stats[ST_ADV * Spad + s], static_cast<unsigned long long>(tot_adv));
+        atomicAdd(&p.stats[ST_SAVE * Spad + s], static_cast<unsigned long long>(tot_save));
+        if (tot_load) atomicAdd(&p.stats[ST_LOAD * Spad + s], static_cast<unsigned long long>(tot_load));
+        if (tot_sel) atomicAdd(&p.stats[ST_SELECT * Spad + s], static_cast<unsigned long long>(tot_sel));
+      }
     }
     if constexpr (kInFan) {
       if (in_fan) {  // the branches' metadata for the next launch's first tick

@@ -66,7 +66,9 @@ rb_status rb_register_game_plugin(const char* path, int32_t* game_id);
 typedef enum rb_request_kind { RB_REQ_SAVE = 0, RB_REQ_LOAD = 1, RB_REQ_ADVANCE = 2 } rb_request_kind;
 
 #define RB_FLAG_CHECKED 1u          /* advance_frame reports MismatchedChecksum synchronously, like the reference (default) */
-#define RB_FLAG_LANE_PER_SESSION 2u /* ex_game: one lane per session instead of one lane per player (tuning/A-B only) */
+#define RB_FLAG_LANE_PER_SESSION 2u /* ex_game: one lane per session instead of one lane per player; only
+                                       libraries built with RB_EXPERIMENTS=1 accept it (the product library
+                                       refuses it at create with RB_INVALID_REQUEST) */
 
 /* SessionBuilder fields used by start_synctest_session (builder.rs:32-52). */
 typedef struct rb_config {
@@ -144,8 +146,8 @@ rb_status rb_advance_frame(rb_batch* b);
  * steady-state ticks (current frame > check_distance, 1 <= check_distance <= 16)
  * execute as ONE fused device launch (for games of at most 80 B of state per
  * cell, e.g. ex_game and the stubs, while the batch's snapshot ring is below
- * 4 GiB: ex_game P=2, W=8 up to 26M sessions; larger rings run one launch per
- * tick, same results).  A session whose resimulation
+ * 4 GiB: ex_game P=2, W=8 holds 40 B per session per slot, 320 B per session,
+ * so up to 13.4M sessions; larger rings run one launch per tick, same results).  A session whose resimulation
  * mismatches stops advancing (as with per-tick calls) while the others run
  * on; with RB_FLAG_CHECKED the call returns RB_MISMATCHED_CHECKSUM if any
  * session has failed by its end.  Bookkeeping errors (RB_INVALID_REQUEST,

@@ -29,7 +29,10 @@ Q = "p2p ex_game P=2 W=8 d=2 rd=2 lag=1,4"
 QB = "p2p brawler P=2 W=8 d=2 rd=2 lag=1,4"
 Q4 = "p2p ex_game P=4 W=8 d=2 rd=2 lag=1,4"
 P2P = "--session p2p"
-# name: (bench args, profiled-run args, profile key, ticks per timed launch)
+# name: (bench args, profiled-run args (unused since round 6), profile key, ticks per timed launch).
+# P2P warm-ups are whole timed launches (multiples of --ticks-per-launch): the warm-up's dispatches
+# of the dominant kernel then have the timed shape too, and the adaptive fan-out sees the same calls
+# whether or not the run is profiled.
 LINES = {
     "driver": ("--gpus 1 --steps 20 --warmup 5", "--steps 20 --warmup 20 --ticks-per-launch 20", f"{X} S=65536 tpl=20", 20),
     "synctest": ("--steps 400 --warmup 32", "--steps 200 --warmup 50", f"{X} S=65536", 50),
@@ -46,7 +49,7 @@ LINES = {
     "brawler": ("--game brawler --steps 100 --warmup 32", "--game brawler --steps 100 --warmup 50", f"{B} S=65536", 50),
     "brawler1": ("--game brawler --ticks-per-launch 1 --steps 32 --warmup 8",
                  "--game brawler --ticks-per-launch 1 --steps 16 --warmup 8", f"{B} S=65536 tpl=1", 1),
-    "p2p": (f"{P2P} --steps 400 --warmup 32", f"{P2P} --steps 200 --warmup 50", f"{Q} S=65536", 50),
+    "p2p": (f"{P2P} --steps 400 --warmup 50", f"{P2P} --steps 200 --warmup 50", f"{Q} S=65536", 50),
     "p2p131k": (f"{P2P} --sessions-per-gpu 131072 --steps 400 --warmup 50",
                 f"{P2P} --sessions-per-gpu 131072 --steps 200 --warmup 50", f"{Q} S=131072", 50),
     "p2p1": (f"{P2P} --ticks-per-launch 1 --steps 400 --warmup 32", f"{P2P} --ticks-per-launch 1 --steps 100 --warmup 32",
@@ -55,23 +58,23 @@ LINES = {
                   f"{P2P} --ticks-per-launch 1 --sessions-per-gpu 131072 --steps 60 --warmup 32", f"{Q} S=131072 tpl=1", 1),
     "p2p1_1m": (f"{P2P} --ticks-per-launch 1 --sessions-per-gpu 1048576 --steps 50 --warmup 16",
                 f"{P2P} --ticks-per-launch 1 --sessions-per-gpu 1048576 --steps 20 --warmup 16", f"{Q} S=1048576 tpl=1", 1),
-    "p2p_sparse": (f"{P2P} --sparse-saving --steps 400 --warmup 32", f"{P2P} --sparse-saving --steps 200 --warmup 50",
+    "p2p_sparse": (f"{P2P} --sparse-saving --steps 400 --warmup 50", f"{P2P} --sparse-saving --steps 200 --warmup 50",
                    f"{Q} S=65536 sparse", 50),
-    "brawler_p2p": (f"--game brawler {P2P} --steps 100 --warmup 32", f"--game brawler {P2P} --steps 100 --warmup 50",
+    "brawler_p2p": (f"--game brawler {P2P} --steps 100 --warmup 50", f"--game brawler {P2P} --steps 100 --warmup 50",
                     f"{QB} S=65536", 50),
-    "brawler_p2p_sparse": (f"--game brawler {P2P} --sparse-saving --steps 100 --warmup 32",
+    "brawler_p2p_sparse": (f"--game brawler {P2P} --sparse-saving --steps 100 --warmup 50",
                            f"--game brawler {P2P} --sparse-saving --steps 100 --warmup 50", f"{QB} S=65536 sparse", 50),
-    "c4": (f"{P2P} --num-players 4 --fanout --steps 100 --warmup 16", f"{P2P} --num-players 4 --fanout --steps 100 --warmup 50",
+    "c4": (f"{P2P} --num-players 4 --fanout --steps 100 --warmup 50", f"{P2P} --num-players 4 --fanout --steps 100 --warmup 50",
            f"{Q4} S=65536 fanout", 50),
-    "c4_pp": (f"{P2P} --num-players 4 --fanout --fanout-mode per-player --steps 100 --warmup 16",
+    "c4_pp": (f"{P2P} --num-players 4 --fanout --fanout-mode per-player --steps 100 --warmup 50",
               f"{P2P} --num-players 4 --fanout --fanout-mode per-player --steps 100 --warmup 50",
               f"{Q4} S=65536 fanout per-player", 50),
-    "c4_k8": (f"{P2P} --num-players 4 --fanout --fanout-k 8 --steps 100 --warmup 16",
+    "c4_k8": (f"{P2P} --num-players 4 --fanout --fanout-k 8 --steps 100 --warmup 50",
               f"{P2P} --num-players 4 --fanout --fanout-k 8 --steps 100 --warmup 50", f"{Q4} S=65536 fanout8", 50),
-    "brawler_fan": (f"--game brawler {P2P} --fanout --steps 20 --warmup 80",
+    "brawler_fan": (f"--game brawler {P2P} --fanout --steps 20 --warmup 100 --ticks-per-launch 20",
                     f"--game brawler {P2P} --fanout --steps 20 --warmup 80", f"{QB} S=65536 fanout tpl=20", 20),
     "wire": (f"{P2P} --wire --steps 200 --warmup 32", f"{P2P} --wire --steps 100 --warmup 16", f"{Q} S=65536 wire tpl=1", 1),
-    "wire_replay": (f"{P2P} --wire-replay --steps 400 --warmup 32", f"{P2P} --wire-replay --steps 200 --warmup 50",
+    "wire_replay": (f"{P2P} --wire-replay --steps 400 --warmup 50", f"{P2P} --wire-replay --steps 200 --warmup 50",
                     f"{Q} S=65536 wire-replay", 50),
 }
 PMC = {
@@ -158,9 +161,7 @@ def copy(tag, names):
 
 if __name__ == "__main__":
     what, tag = sys.argv[1], sys.argv[2]
-    # (brawler_fan mixes one-tick fan-out launches and, once the adaptive fan-out has paused,
-    # 20-tick plain ones in one run: no per-launch profile describes it)
-    names = sys.argv[3:] or [n for n in LINES if not (what in ("prof", "fold") and n == "brawler_fan")]
+    names = sys.argv[3:] or list(LINES)
     bad = [n for n in names if n not in LINES]
     if bad:
         raise SystemExit(f"unknown lines {bad}; known: {list(LINES)}")

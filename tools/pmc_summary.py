@@ -83,8 +83,19 @@ def main():
                 # steady launches of the measured shape: drop the warm-up launch (first)
                 v = vals[1:] if len(vals) > 1 else vals
                 ent[c] = sum(v) / len(v)
-    # the dominant kernel: the fused steady / P2P kernel of the bench line
+    # the dominant kernel: the fused steady / P2P kernel of the bench line; with the run's meta, among
+    # the kernels of its timed launches (the trace's last dispatches, one per clock span)
     steady = [k for k in summary["kernels"] if "steady_kernel" in k or "p2p_kernel" in k or "fanout" in k]
+    spans0 = meta.get("clock_spans_us")
+    traces0 = find(os.path.join(d, "stats"), "*kernel_trace.csv")
+    if spans0 and traces0:
+        with open(traces0[0]) as f:
+            rows0 = [r for r in csv.DictReader(f) if short(r["Kernel_Name"]) in steady]
+        rows0.sort(key=lambda r: int(r["Start_Timestamp"]))
+        timed = {short(r["Kernel_Name"]) for r in rows0[-len(spans0):]}
+        if timed:
+            steady = [k for k in steady if k in timed]
+            summary["timed_kernels"] = sorted(timed)
     if steady:
         k = max(steady, key=lambda n: summary["kernels"][n].get("total_ns", 0.0))
         e = summary["kernels"][k]
@@ -139,11 +150,9 @@ def main():
             rows = [r for r in csv.DictReader(f) if ("p2p_kernel" in r["Kernel_Name"] or "steady_kernel" in r["Kernel_Name"]
                                                      or "fanout_kernel" in r["Kernel_Name"])]
         rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-        dom = summary["dominant_kernel"]
         # timed launches = the trace's last len(spans) dispatches of the kernel(s) the clock covers
-        # (with GGRS_BENCH_PROFILE=1 the warm-up ran other kernels; the two-launch fan-out
-        # alternates p2p_kernel and fanout_kernel)
-        cand = [r for r in rows if short(r["Kernel_Name"]) == dom or "fanout_kernel" in r["Kernel_Name"]]
+        # (the two-launch fan-out alternates p2p_kernel and fanout_kernel)
+        cand = rows
         if len(cand) >= len(spans):
             cand = cand[-len(spans):]
             dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in cand]
