@@ -321,9 +321,13 @@ struct P2PParams {
   // speculative fan-out (spec_on = 0: plain P2P).  fanout_kernel (below, a
   // launch of its own between one-tick P2P launches): branch-major columns
   // (s * kSpecBranches + k) * L + lane, so one session's 16 branches x L lanes
-  // store 64 consecutive words per plane.  The in-kernel fan-out (kInFan):
-  // column s * kSpecBranches + k of planes Spad * 16 wide, the speculated
-  // player's words only.
+  // store 64 consecutive words per plane.  The in-kernel fan-out (kInFan),
+  // the speculated player's words only: branch k in plane k / L at column
+  // (k / L) * Spad * L + s * L + lane (the lane that runs it), the other
+  // players' own chains at Spad * 16 + s * L + lane (planes Spad * (16 + L)
+  // wide); the per-player form: class k of lane l's player at k * Spad * L +
+  // s * L + l, a local player's chain at 16 * Spad * L + s * L + l (planes
+  // Spad * L * 17 wide).  Every chain slot of a wave stores 64 consecutive words.
   uint32_t* spec_state;  // [NW planes][Spad*16*L] branch states at meta end
   uint32_t* spec_cells;  // [W][NW planes][Spad*16*L] branch cells
   const void* spec_cs;   // [W][Spad][16] CS (fanout_kernel)
@@ -1174,9 +1178,9 @@ p2p_kernel(const P2PParams p) {
         ok &= kk >= 0;
       }
       const unsigned Gs = Spad * static_cast<unsigned>(L) * static_cast<unsigned>(kSpecBranches + 1);
-      const unsigned col = my_remote ? (s * static_cast<unsigned>(L) + static_cast<unsigned>(lane)) * kSpecBranches +
-                                           static_cast<unsigned>(kk >= 0 ? kk : 0)
-                                     : Spad * static_cast<unsigned>(L) * kSpecBranches + s * L + static_cast<unsigned>(lane);
+      // (fan_per_player's columns: class kk of lane l's player at kk * Spad * L + s * L + l)
+      const unsigned col = (my_remote ? static_cast<unsigned>(kk >= 0 ? kk : 0) : static_cast<unsigned>(kSpecBranches)) *
+                               (Spad * static_cast<unsigned>(L)) + s * L + static_cast<unsigned>(lane);
       const bool has = lane < P;
       if (F > B && ok && has) {  // the branch at F must be the cell the reference loads
         const unsigned fslot = static_cast<unsigned>(F % W);
@@ -1269,14 +1273,16 @@ p2p_kernel(const P2PParams p) {
     exec = true;
     if (status == kP2PStatusPanic) return true;
     if (in_fan) {
-      // the in-kernel fan-out's branch kk: column s * 16 + kk, written by lane (rs + kk) % L (which alone reads
+      // the in-kernel fan-out's branch kk, written by lane (rs + kk) % L (which alone reads
       // it back and hands the words to the speculated player's lane); every other lane keeps its own
       // cells and state (no misprediction of its player), and each cell's checksum is rebuilt from the
       // players' fletcher parts
       if constexpr (kInFan) {
         const unsigned Gs = Spad * static_cast<unsigned>(kSpecBranches + L);
         const int owner = (rs + kk) % static_cast<int>(L);  // (fan_inlane's deal of branches to lanes)
-        const unsigned col = s * kSpecBranches + static_cast<unsigned>(kk);
+        // (fan_inlane's columns: branch kk in plane kk / L, the owner lane's column there)
+        const unsigned col = static_cast<unsigned>(kk / static_cast<int>(L)) * (Spad * static_cast<unsigned>(L)) + s * L +
+                             static_cast<unsigned>(owner);
         const unsigned ocol = Spad * kSpecBranches + s * L + static_cast<unsigned>(lane);  // this lane's player, once
         const bool other = lane < P && lane != rs;
         const int src = static_cast<int>(__lane_id()) - lane + owner;
@@ -1786,8 +1792,8 @@ p2p_kernel(const P2PParams p) {
   // (confirmed inputs up to its own last added frame, then the class held), each local player's
   // lane its player once with its confirmed inputs.  A later tick whose rollback starts at B and
   // in which every remote player's newly confirmed inputs hold one class (or none arrived) then
-  // selects, player by player (try_select).  Columns: branch k of lane l's player (s * L + l) * 16
-  // + k, a local player's chain Spad * L * 16 + s * L + l (planes Spad * L * 17 wide).
+  // selects, player by player (try_select).  Columns: class k of lane l's player k * Spad * L + s * L
+  // + l, a local player's chain Spad * L * 16 + s * L + l (planes Spad * L * 17 wide).
   auto fan_per_player = [&]() __attribute__((always_inline)) {
     if constexpr (kInFan && !kMtf) {
       const int lane_base = static_cast<int>(__lane_id()) - lane;
@@ -1830,7 +1836,10 @@ p2p_kernel(const P2PParams p) {
       fan_prefetch(ring, h_own, s, B, cur, own_local, la_own, pred_own, vin);
       const uint64_t vpk = fan_pack(vin);
       const unsigned Gs = Spad * static_cast<unsigned>(L) * static_cast<unsigned>(kSpecBranches + 1);
-      const unsigned bcol = (s * static_cast<unsigned>(L) + static_cast<unsigned>(lane)) * kSpecBranches;
+      // class k of this lane's player at column k * Spad * L + s * L + lane: one chain slot of the whole
+      // wave stores 64 consecutive words per plane (with the columns (s * L + lane) * 16 + k of round 5 a
+      // store wrote 4 bytes of every 64-byte line: the per-player C4 tick spent 21 of its 61 us storing)
+      const unsigned bcol = s * static_cast<unsigned>(L) + static_cast<unsigned>(lane);
       const unsigned ocol = Spad * static_cast<unsigned>(L) * kSpecBranches + s * L + static_cast<unsigned>(lane);
       const int nsl = my_remote ? nb : (lane < P ? 1 : 0);  // this lane's chains
       bool inr = false;
@@ -1855,7 +1864,7 @@ p2p_kernel(const P2PParams p) {
           const int k = b0 + b;
           on[b] = k < nsl;
           rep[b] = cand_at(acp, k & (kSpecBranches - 1));
-          col[b] = my_remote ? bcol + static_cast<unsigned>(k & (kSpecBranches - 1)) : ocol;
+          col[b] = my_remote ? static_cast<unsigned>(k & (kSpecBranches - 1)) * (Spad * static_cast<unsigned>(L)) + bcol : ocol;
 #pragma unroll
           for (int n = 0; n < NW; ++n) wb[b][n] = ow[n];
         }
@@ -2020,7 +2029,11 @@ p2p_kernel(const P2PParams p) {
           own[b] = b == NG - 1 && last && other;
           any_own |= own[b];
           in[b] = static_cast<InRec>(static_cast<uint64_t>(cand_at(cand, k & (kSpecBranches - 1))) << (8 * rs));
-          col[b] = own[b] ? ocol : s * kSpecBranches + static_cast<unsigned>(k & (kSpecBranches - 1));
+          // branch k in plane k / L (this lane's column there): a chain slot of the wave stores 64
+          // consecutive words per plane (round 5's columns s * 16 + k filled 16 of every 64 bytes)
+          col[b] = own[b] ? ocol
+                          : static_cast<unsigned>((k & (kSpecBranches - 1)) / static_cast<int>(L)) * (Spad * static_cast<unsigned>(L)) +
+                                s * L + static_cast<unsigned>(lane);
 #pragma unroll
           for (int n = 0; n < NW; ++n) wb[b][n] = own[b] ? ow[n] : bw[n];
         }
