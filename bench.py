@@ -169,11 +169,16 @@ def measured_copy_gbps(dev, nbytes=1 << 30, iters=10):
     return gbps
 
 
-def source_id():
+P2P_ONLY_SOURCES = ("p2p.hpp", "p2p_engine.hip", "wire.hip")
+
+
+def source_id(family="p2p"):
     """Identity of the device code a profile describes: a hash of the kernel sources, the
     header and the build flags (ggrs_amd/csrc/*.hip, *.hpp, Makefile, include/*), the same
     for every build of the same sources.  A PMC profile is used only for the sources it was
-    taken on."""
+    taken on.  The SyncTest family ("synctest") leaves out the sources only the P2P batches
+    compile into their kernels (P2P_ONLY_SOURCES: p2p_kernel, the fan-out, the wire codec),
+    so a P2P change does not orphan the SyncTest profiles."""
     import glob
     import hashlib
     h = hashlib.sha256()
@@ -181,6 +186,8 @@ def source_id():
                    glob.glob(os.path.join(ROOT, "ggrs_amd", "csrc", "*.hpp")) +
                    [os.path.join(ROOT, "ggrs_amd", "csrc", "Makefile")] +
                    glob.glob(os.path.join(ROOT, "include", "*.h*")))
+    if family == "synctest":
+        files = [f for f in files if os.path.basename(f) not in P2P_ONLY_SOURCES]
     for f in files:
         h.update(os.path.basename(f).encode())
         with open(f, "rb") as fh:
@@ -188,7 +195,7 @@ def source_id():
     return h.hexdigest()[:16]
 
 
-def pmc_profile(cfg_key, fanout_state=None):
+def pmc_profile(cfg_key, fanout_state=None, family="p2p"):
     """The committed rocprofv3 PMC summary of this exact configuration and launch shape
     (profiles/*pmc*.json, written by tools/pmc_summary.py), taken on the current kernel
     sources (`source_id`) and, for a fan-out line, with the fan-out in the same state
@@ -198,16 +205,19 @@ def pmc_profile(cfg_key, fanout_state=None):
     engine's access widths by tools/calib_fetch.hip); its `issue` block holds SQ_INSTS_VALU,
     the clock and the VALU issue-slot fraction."""
     import glob
-    src = source_id()
+    src = source_id(family)
     best = None
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
+    if os.environ.get("GGRS_PROFILES_OUT"):  # (tools/lines.py line: this call's own profiles, folded on the box)
+        paths += sorted(glob.glob(os.path.join(os.environ["GGRS_PROFILES_OUT"], "*pmc*.json")))
+    for path in paths:
         try:
             d = json.load(open(path))
         except Exception:
             continue
         if (d.get("config_key") == cfg_key and d.get("hbm_bytes_per_tick") and d.get("source_id") == src
                 and (fanout_state is None or d.get("fanout_state") == fanout_state)):
-            best = dict(d, file=os.path.relpath(path, ROOT))
+            best = dict(d, file="profiles/" + os.path.basename(path))
     return best
 
 
@@ -221,11 +231,15 @@ def dispatch_overhead_us(cfg_key=None):
     under rocprofv3 --kernel-trace and pairing every timed dispatch with its clock span
     (tools/clock_calib.py -> profiles/r06_clock_calibration.json): the median of this line's
     configuration when it was profiled, else the median over all lines; (0, None) when absent."""
+    path = CLOCK_CAL_FILE
+    out = os.environ.get("GGRS_PROFILES_OUT")  # (tools/lines.py line: this call's own calibration)
+    if out and os.path.exists(os.path.join(out, os.path.basename(CLOCK_CAL_FILE))):
+        path = os.path.join(out, os.path.basename(CLOCK_CAL_FILE))
     try:
-        d = json.load(open(CLOCK_CAL_FILE))
+        d = json.load(open(path))
         by = d.get("by_config", {})
         v = by[cfg_key] if cfg_key in by else d["dispatch_overhead_us"]
-        return float(v), os.path.relpath(CLOCK_CAL_FILE, ROOT)
+        return float(v), "profiles/" + os.path.basename(path)
     except (OSError, KeyError, ValueError):
         return 0.0, None
 
@@ -1055,11 +1069,11 @@ def main():
                                    (" (fused steady-state ticks)" if tpl > 1 else " (one tick per launch)"))
                                   if fused else (f"tick_kernel<{'Brawler' if brawler else 'ExGame'}<{P}>> (one launch "
                                                  f"per tick: no fused kernel past check distance 16)"),
-                                  pmc_profile(cfg_key), model, copy_gbps)
+                                  pmc_profile(cfg_key, family="synctest"), model, copy_gbps)
         roofline.update(timer)
         roofline["algorithmic_bytes_per_session_tick"] = bpt
         roofline["measured_copy_GBps"] = copy_gbps
-        write_meta(config_key=cfg_key, source_id=source_id(), fanout_state=None, kernel="steady_kernel",
+        write_meta(config_key=cfg_key, source_id=source_id("synctest"), fanout_state=None, kernel="steady_kernel",
                    clock_spans_us=spans, dispatch_overhead_us=timer.get("dispatch_overhead_us"),
                    kernel_avg_us=avg_kernel_s * 1e6, bytes_per_launch=bytes_per_launch)
         if brawler:

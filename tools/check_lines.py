@@ -1,0 +1,58 @@
+"""Recompute every bench line's roofline fraction from its committed rocprofv3 summary (VERDICT r05
+"next" 1): algorithmic bytes per timed launch (the line's roofline.algorithmic_bytes_per_launch) over
+the AverageNs of the line's dominant kernel in profiles/TAG_NAME_kernel_stats.csv (its every
+dispatch is a timed launch of the line's shape: GGRS_BENCH_PROFILE=1 and whole-launch warm-ups),
+against the 8 TB/s spec; and the line's PMC traffic against the measured copy ceiling.
+
+    python3 tools/check_lines.py r06 [DIR]     # DIR: where bench_TAG_*.jsonl and the summaries are
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    tag = sys.argv[1]
+    d = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "profiles")
+    worst = 0.0
+    print(f"{'line':22s} {'frac':>7s} {'recomputed':>10s} {'diff':>7s} {'kernel_us':>10s} {'rocprof_us':>10s} "
+          f"{'calls':>5s} {'dram/ceil':>9s} bound")
+    for path in sorted(glob.glob(os.path.join(d, f"bench_{tag}_*.jsonl"))):
+        name = os.path.basename(path)[len(f"bench_{tag}_"):-len(".jsonl")]
+        line = json.loads(open(path).readline())
+        r = line["roofline"]
+        pmc = os.path.join(d, f"{tag}_{name}_pmc.json")
+        if not os.path.exists(pmc):
+            print(f"{name:22s} no profile")
+            continue
+        p = json.load(open(pmc))
+        k = p.get("dominant_kernel")
+        stats = os.path.join(d, f"{tag}_{name}_kernel_stats.csv")
+        avg, calls = None, 0
+        for row in csv.DictReader(open(stats)):
+            if row["Name"].split("(")[0].replace("void ", "").strip() == k:
+                avg, calls = float(row["AverageNs"]), int(row["Calls"])
+        per_launch = r["algorithmic_bytes_per_launch"]
+        if p.get("tick_kernels") or (len(p.get("timed_kernels", [])) > 1):
+            # two kernels per tick: the stats' per-dispatch averages of both, per tick
+            tot = 0.0
+            for row in csv.DictReader(open(stats)):
+                n = row["Name"].split("(")[0].replace("void ", "").strip()
+                if n in p.get("timed_kernels", []):
+                    tot += float(row["AverageNs"])
+            avg = tot
+        rec = per_launch / (avg * 1e-9) / 1e9 / 8000.0
+        diff = rec / r["frac"] - 1.0
+        worst = max(worst, abs(diff))
+        dc = r.get("dram_frac_of_ceiling")
+        print(f"{name:22s} {r['frac']:7.3f} {rec:10.3f} {100 * diff:6.1f}% {r['kernel_avg_us']:10.2f} {avg / 1e3:10.2f} "
+              f"{calls:5d} {dc if dc is None else round(dc, 2)!s:>9s} {r['bound']}")
+    print(f"worst |diff| {100 * worst:.1f}%")
+
+
+if __name__ == "__main__":
+    main()

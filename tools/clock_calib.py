@@ -20,21 +20,24 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def main():
     tag = sys.argv[1]
+    prof = os.environ.get("GGRS_PROFILES_OUT") or os.path.join(ROOT, "profiles")
     by, rows = {}, []
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"{tag}_*_pmc.json"))):
+    for path in sorted(glob.glob(os.path.join(prof, f"{tag}_*_pmc.json"))):
         d = json.load(open(path))
         c = d.get("clock_vs_rocprof")
         if not c:
             continue
-        by[d["config_key"]] = round(c["overhead_median_us"], 3)
-        rows.append({"profile": os.path.relpath(path, ROOT), "config_key": d["config_key"], **c})
+        # the mean difference: the line's clock average plus it is then its dispatches' rocprofv3 average
+        # (the --stats AverageNs a recomputation starts from)
+        by[d["config_key"]] = round(c["rocprof_avg_us"] - c["clock_avg_us"], 3)
+        rows.append({"profile": "profiles/" + os.path.basename(path), "config_key": d["config_key"], **c})
     if not rows:
         raise SystemExit("no profile with clock_vs_rocprof")
     med = sorted(by.values())[len(by) // 2]
     out = {"what": "rocprofv3 dispatch duration minus the kernel's own clock span (first wave start to last wave "
                    "end), per timed dispatch of each profiled bench line, median per line; bench.py adds it to "
                    "the clock spans it measures", "dispatch_overhead_us": med, "by_config": by, "lines": rows}
-    with open(os.path.join(ROOT, "profiles", f"{tag}_clock_calibration.json"), "w") as f:
+    with open(os.path.join(prof, f"{tag}_clock_calibration.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps({"dispatch_overhead_us": med, "lines": len(rows)}))
 

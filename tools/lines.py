@@ -8,6 +8,8 @@
     python3 tools/lines.py fold TAG [NAME ...]    # here: profiles/TAG_NAME_{kernel_stats.csv,pmc.json}
                                                   # (tools/pmc_summary.py), keyed like bench.py's lookup
     python3 tools/lines.py copy TAG [NAME ...]    # here: gpurun_out/bench_TAG_* -> profiles/
+    python3 tools/lines.py line TAG [NAME ...]    # GPU box: per line prof, fold (into gpurun_out/prof_TAG),
+                                                  # clock calibration, then the bench run
 
 Each line: the bench.py arguments of the bench run, (unused since round 6: the profiled run is
 the bench run's own command), bench.py's profile key for it and the ticks per timed launch.
@@ -138,6 +140,25 @@ def prof(tag, names):
     return 0
 
 
+def line(tag, names):
+    """GPU box: per line, the profiled runs, their fold into GGRS_PROFILES_OUT (default
+    gpurun_out/prof_TAG), the clock calibration over the lines profiled so far, then the bench
+    run, which reads that calibration and profile: the line and the profile it is checked
+    against come from the same box, minutes apart."""
+    out = os.environ.setdefault("GGRS_PROFILES_OUT", os.path.join(ROOT, "gpurun_out", f"prof_{tag}"))
+    os.makedirs(out, exist_ok=True)
+    for n in names:
+        if prof(tag, [n]) != 0:
+            return 1
+        subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_summary.py"),
+                        os.path.join(ROOT, "gpurun_out", f"prof_{tag}_{n}"), f"{tag}_{n}", LINES[n][2], str(LINES[n][3])],
+                       check=True, stdout=subprocess.DEVNULL)
+        subprocess.run([sys.executable, os.path.join(ROOT, "tools", "clock_calib.py"), tag], check=True)
+        if bench(tag, [n]) != 0:
+            return 1
+    return 0
+
+
 def fold(tag, names):
     for n in names:
         d = os.path.join(ROOT, "gpurun_out", f"prof_{tag}_{n}")
@@ -165,4 +186,4 @@ if __name__ == "__main__":
     bad = [n for n in names if n not in LINES]
     if bad:
         raise SystemExit(f"unknown lines {bad}; known: {list(LINES)}")
-    sys.exit({"bench": bench, "prof": prof, "fold": fold, "copy": copy}[what](tag, names))
+    sys.exit({"bench": bench, "prof": prof, "fold": fold, "copy": copy, "line": line}[what](tag, names))

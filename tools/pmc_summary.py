@@ -57,7 +57,7 @@ def main():
     d, tag = sys.argv[1], sys.argv[2]
     cfg_key = sys.argv[3] if len(sys.argv) > 3 else "ex_game P=2 cd=7 W=8 d=2 S=65536"
     tpl = int(sys.argv[4]) if len(sys.argv) > 4 else 50
-    prof = os.path.join(ROOT, "profiles")
+    prof = os.environ.get("GGRS_PROFILES_OUT") or os.path.join(ROOT, "profiles")  # (the GPU box: under gpurun_out)
     os.makedirs(prof, exist_ok=True)
     stats = find(os.path.join(d, "stats"), "*kernel_stats.csv")
     summary = {"tag": tag, "config_key": cfg_key, "ticks_per_launch": tpl, "kernels": {}}
