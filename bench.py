@@ -286,18 +286,23 @@ def roofline_block(bytes_per_launch, avg_kernel_s, ticks_per_launch, launches, k
     profiles/r02_calib_write.json), "valu" when the VALU issue slots are above 0.7 busy,
     "latency" (dependent chains at low occupancy) otherwise; "unprofiled"
     when no PMC profile of this configuration is committed, or when the profile's traffic
-    over this kernel time would exceed the measured copy ceiling (`copy_gbps`): counters
-    that describe other launches than the ones timed here are refused, not reported."""
+    over this kernel time would exceed the fastest rate DRAM was measured to take (the copy
+    `copy_gbps` or the calibrated store-only ceiling): counters that describe other launches
+    than the ones timed here are refused, not reported."""
     achieved = bytes_per_launch / avg_kernel_s / 1e9
     r = {"bound": "unprofiled", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
          "frac": achieved / HBM_PEAK_GBS, "frac_basis": "algorithmic bytes / kernel time / 8 TB/s HBM spec",
          "traffic": None, "dram_frac": None, "algorithmic_bytes_per_launch": bytes_per_launch, "bytes_model": model,
          "kernel_avg_us": avg_kernel_s * 1e6, "ticks_per_launch": ticks_per_launch, "launches_timed": launches,
          "kernel": kernel}
-    if prof and copy_gbps and prof["hbm_bytes_per_tick"] * ticks_per_launch / avg_kernel_s / 1e9 > copy_gbps:
+    # the fastest rate DRAM was measured to take on this engine's patterns: the device-to-device copy
+    # (read + write) or the calibrated store-only stream, whichever is higher
+    ceiling = max(copy_gbps or 0.0, store_ceiling_gbps() or 0.0) or None
+    if prof and ceiling and prof["hbm_bytes_per_tick"] * ticks_per_launch / avg_kernel_s / 1e9 > ceiling:
         r["pmc_refused"] = (f"{prof['file']}: its traffic over this kernel time would be "
                             f"{prof['hbm_bytes_per_tick'] * ticks_per_launch / avg_kernel_s / 1e9:.0f} GB/s, above the "
-                            f"measured {copy_gbps:.0f} GB/s copy ceiling")
+                            f"{ceiling:.0f} GB/s measured ceiling (copy {copy_gbps or 0:.0f}, store-only "
+                            f"{store_ceiling_gbps() or 0:.0f})")
         prof = None
     if prof:
         traffic = prof["hbm_bytes_per_tick"] * ticks_per_launch

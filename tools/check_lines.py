@@ -2,7 +2,9 @@
 "next" 1): algorithmic bytes per timed launch (the line's roofline.algorithmic_bytes_per_launch) over
 the AverageNs of the line's dominant kernel in profiles/TAG_NAME_kernel_stats.csv (its every
 dispatch is a timed launch of the line's shape: GGRS_BENCH_PROFILE=1 and whole-launch warm-ups),
-against the 8 TB/s spec; and the line's PMC traffic against the measured copy ceiling.
+against the 8 TB/s spec; next to it the line's kernel time as clock span + calibrated dispatch overhead
+and the range of (rocprofv3 duration - clock span) over the profiled run's timed dispatches (the same
+process as the summary): what is left of a difference is the kernel's run-to-run spread.
 
     python3 tools/check_lines.py r06 [DIR]     # DIR: where bench_TAG_*.jsonl and the summaries are
 """
@@ -20,7 +22,7 @@ def main():
     d = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "profiles")
     worst = 0.0
     print(f"{'line':22s} {'frac':>7s} {'recomputed':>10s} {'diff':>7s} {'kernel_us':>10s} {'rocprof_us':>10s} "
-          f"{'calls':>5s} {'dram/ceil':>9s} bound")
+          f"{'calls':>5s} {'clock+ovh_us':>12s} {'ovh range_us':>13s} {'dram/ceil':>9s} bound")
     for path in sorted(glob.glob(os.path.join(d, f"bench_{tag}_*.jsonl"))):
         name = os.path.basename(path)[len(f"bench_{tag}_"):-len(".jsonl")]
         line = json.loads(open(path).readline())
@@ -49,8 +51,13 @@ def main():
         diff = rec / r["frac"] - 1.0
         worst = max(worst, abs(diff))
         dc = r.get("dram_frac_of_ceiling")
+        # the profiled run's dispatches paired with their own clock spans (same process: no run-to-run
+        # spread): the spread of rocprofv3 duration minus clock span over the timed dispatches
+        cv = p.get("clock_vs_rocprof") or {}
+        rng = f"{cv.get('overhead_min_us', 0):.2f}-{cv.get('overhead_max_us', 0):.2f}" if cv else "-"
         print(f"{name:22s} {r['frac']:7.3f} {rec:10.3f} {100 * diff:6.1f}% {r['kernel_avg_us']:10.2f} {avg / 1e3:10.2f} "
-              f"{calls:5d} {dc if dc is None else round(dc, 2)!s:>9s} {r['bound']}")
+              f"{calls:5d} {r.get('kernel_clock_us', 0):7.2f}+{r.get('dispatch_overhead_us') or 0:4.2f} {rng:>13s} "
+              f"{dc if dc is None else round(dc, 2)!s:>9s} {r['bound']}")
     print(f"worst |diff| {100 * worst:.1f}%")
 
 

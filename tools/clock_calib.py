@@ -5,8 +5,8 @@
 Every profiled line (tools/lines.py prof, GGRS_BENCH_PROFILE=1) ran its own command under
 rocprofv3 --kernel-trace; tools/pmc_summary.py paired each timed dispatch's rocprofv3 duration
 with the kernel's own clock span of the same launch (rb_launch_clock_*: first wave start to last
-wave end on the 100 MHz constant clock) and kept the median difference per line.  That
-difference is the dispatch's setup before the first wave plus its end-of-kernel release after the
+wave end on the 100 MHz constant clock); the line's overhead is the mean difference.  It
+is the dispatch's setup before the first wave plus its end-of-kernel release after the
 last: bench.py adds it, per launch, to the clock span of the launches it times (by the line's
 configuration, else the median over all lines), so that its kernel time is rocprofv3's.
 """
@@ -35,8 +35,8 @@ def main():
         raise SystemExit("no profile with clock_vs_rocprof")
     med = sorted(by.values())[len(by) // 2]
     out = {"what": "rocprofv3 dispatch duration minus the kernel's own clock span (first wave start to last wave "
-                   "end), per timed dispatch of each profiled bench line, median per line; bench.py adds it to "
-                   "the clock spans it measures", "dispatch_overhead_us": med, "by_config": by, "lines": rows}
+                   "end), per timed dispatch of each profiled bench line, the mean per line (by_config; the median "
+                   "over lines for a configuration not profiled); bench.py adds it to the clock spans it measures", "dispatch_overhead_us": med, "by_config": by, "lines": rows}
     with open(os.path.join(prof, f"{tag}_clock_calibration.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps({"dispatch_overhead_us": med, "lines": len(rows)}))
