@@ -56,6 +56,6 @@
 
 /* ABI of the plugin entry points (rb_plugin_abi); bump when the engine's
  * kernel parameter structs change. */
-#define RB_PLUGIN_ABI 5
+#define RB_PLUGIN_ABI 6
 
 #endif /* GGRS_AMD_GAME_HPP */
