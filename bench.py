@@ -463,9 +463,11 @@ def bench_p2p(args):
          .with_num_players(P).with_max_prediction_window(W).with_input_delay(args.input_delay)
          .with_remote_input_delay(args.remote_delay).with_sparse_saving_mode(args.sparse_saving)
          .with_block_size(args.block_size)
-         .with_speculative_fanout(args.fanout, K, per_player=args.fanout_mode == "per-player"))
+         .with_speculative_fanout(args.fanout, K, per_player=None if args.fanout_mode == "auto" else
+                                  args.fanout_mode == "per-player"))
     for h in range(P):
         b.add_player(PlayerType.Local if (mask >> h) & 1 else PlayerType.Remote, h)
+    per_player_mode = b._per_player_resolved()
     stream = torch.cuda.Stream(device=dev)
     # Timing as the SyncTest path (GGRS_BENCH_EVENTS): the kernel's own clock on every timed launch by
     # default.  The warm-up runs in the timed region's call sizes whether or not the run is profiled:
@@ -635,7 +637,7 @@ def bench_p2p(args):
             fan_state = "active" if branch > 0 else "paused"
         cfg_key = (f"p2p {args.game} P={P} W={W} d={args.input_delay} rd={args.remote_delay} lag={lo},{hi} S={S}"
                    + (" sparse" if args.sparse_saving else "") + (f" fanout{'' if K == 16 else K}" if args.fanout else "")
-                   + (" per-player" if args.fanout and args.fanout_mode == "per-player" else "")
+                   + (" per-player" if args.fanout and per_player_mode else "")
                    + (" wire" if args.wire else "") + (" wire-replay" if args.wire_replay else ""))
         tl = int(round(args.steps / max(1, launches)))  # the PMC profile of the launch shape timed here
         cfg_key += f" tpl={tl}" if tl != 50 else ""
@@ -680,7 +682,8 @@ def bench_p2p(args):
                        "advance_frames_per_session_tick": adv / (S * world * args.steps),
                        "rollbacks_per_session_tick": (loads + selects) / (S * world * args.steps),
                        "speculative": ({"branches": K, "alphabet": 16 if not brawler else 256,
-                                        "mode": args.fanout_mode,
+                                        "mode": ("per-player" if per_player_mode else "single") +
+                                                (" (auto)" if args.fanout_mode == "auto" else ""),
                                         "candidates": "whole alphabet" if (not brawler and K >= 16) else
                                                       "the K most recently added distinct inputs (the queue's "
                                                       "move-to-front list), then the smallest values",
@@ -759,9 +762,10 @@ def main():
     ap.add_argument("--fanout", action="store_true",
                     help="p2p: speculative fan-out, --fanout-k candidate inputs per session per tick (BASELINE "
                          "configs[3]; use with --num-players 4)")
-    ap.add_argument("--fanout-mode", choices=["single", "per-player"], default="single",
+    ap.add_argument("--fanout-mode", choices=["auto", "single", "per-player"], default="auto",
                     help="p2p --fanout: speculate the remote player with the oldest unconfirmed input (single) or "
-                         "every remote player (per-player, RB_P2P_FLAG_FANOUT_PER_PLAYER; whole alphabet only)")
+                         "every remote player (per-player, RB_P2P_FLAG_FANOUT_PER_PLAYER; whole alphabet only); "
+                         "auto (default) = per-player for ex_game at K = 16, else single")
     ap.add_argument("--fanout-k", type=int, default=16,
                     help="p2p --fanout: candidates per session (1..16): ex_game's whole alphabet at 16, else the "
                          "most likely K")

@@ -458,12 +458,57 @@ struct ExGame {
     fl16_word(a, w[4], wp(off_rot(i)));
     return a;
   }
+  // The per-player fan-out's shared rotation (p2p.hpp fan_per_player, FanShare): a player's input
+  // classes that turn alike (class bits 2-3) share the rotation and its sine / cosine over the
+  // frames they hold, so one AdvanceFrame splits into fan_turn (once per turn group and frame) and
+  // fan_move (per class).  Each is advance_player's operations on the same operands: bit-identical.
+  static constexpr bool kFanShare = kSplit;
+  template <bool kInRange>
+  __device__ static float fan_turn(float rot, uint32_t cls) {  // the rotation after the frame (:291-296)
+    const bool left = cls & 4u, right = cls & 8u;
+    const float r1 = rem_euclid<kInRange>(left ? rot - kRotationSpeed : rot + kRotationSpeed, 2.0f * kPi);
+    return left != right ? r1 : rot;
+  }
+  // friction, thrust (tx, ty = MOVEMENT_SPEED * (cos, sin)(rotation before the frame)), speed clamp
+  // and position (:277-289, :298-314) of one player's words; the rotation word is the caller's
+  __device__ static void fan_move(uint32_t* w, float tx, float ty, uint32_t cls) {
+    const float old_x = __uint_as_float(w[0]), old_y = __uint_as_float(w[1]);
+    float vx = __uint_as_float(w[2]) * kFriction;
+    float vy = __uint_as_float(w[3]) * kFriction;
+    const bool up = cls & 1u, down = cls & 2u;
+    const float vx1 = up ? vx + tx : vx - tx, vy1 = up ? vy + ty : vy - ty;
+    vx = up != down ? vx1 : vx;
+    vy = up != down ? vy1 : vy;
+    speed_clamp(vx, vy);
+    float x = old_x + vx, y = old_y + vy;
+    x = fminf(fmaxf(x, 0.0f), kWidth);
+    y = fminf(fmaxf(y, 0.0f), kHeight);
+    w[0] = __float_as_uint(x);
+    w[1] = __float_as_uint(y);
+    w[2] = __float_as_uint(vx);
+    w[3] = __float_as_uint(vy);
+  }
+  template <bool kInRange>
+  __device__ static SinCos fan_thrust(float rot, uint32_t* unexpected) {  // MOVEMENT_SPEED * (cos, sin)(rot)
+    const SinCos sc = sincosf_glibc<kInRange>(rot, unexpected);
+    return SinCos{kMovementSpeed * sc.s, kMovementSpeed * sc.c};
+  }
   __device__ static CS fan_finish(Fl16 a, int32_t frame) {  // + the constant bytes and the frame word
     a.s1 += kCsC1;
     a.s2 += kCsC2;
     fl16_word(a, static_cast<uint32_t>(frame), fl16_weights(kImageBytes, 0));
     return fl16_finish(a);
   }
+};
+
+// G::kFanShare (ExGame::fan_turn / fan_move / fan_thrust), false for a game that does not declare it
+template <class G, class = void>
+struct FanShare {
+  static constexpr bool value = false;
+};
+template <class G>
+struct FanShare<G, std::void_t<decltype(G::kFanShare)>> {
+  static constexpr bool value = G::kFanShare;
 };
 
 // G::kIndependentPlayers, false for a game that does not declare it

@@ -251,6 +251,13 @@ struct AlphabetClasses {
   }
   static constexpr T value = make();
 };
+// The index of class value c in an AlphabetClasses list (-1: absent), at compile time
+template <class T>
+__host__ __device__ constexpr int class_slot(const T& t, uint32_t c) {
+  for (int i = 0; i < t.n; ++i)
+    if (((t.packed[i >> 2] >> (8 * (i & 3))) & 0xFFu) == c) return i;
+  return -1;
+}
 // The values v < 64 that represent their class (canon(v) == v): what the fill of a class list
 // may add (every value for a game without classes).
 template <class G>
@@ -1178,14 +1185,20 @@ p2p_kernel(const P2PParams p) {
         ok &= kk >= 0;
       }
       const unsigned Gs = Spad * static_cast<unsigned>(L) * static_cast<unsigned>(kSpecBranches + 1);
-      // (fan_per_player's columns: class kk of lane l's player at kk * Spad * L + s * L + l)
+      // (fan_per_player's columns: class kk of lane l's player at kk * Spad * L + s * L + l; with FanShare
+      // a remote player's cells up to frame P0, where its classes still agree, in the lane's own
+      // column 16 * Spad * L + s * L + l, which a local player's chain uses for all of its cells)
       const unsigned col = (my_remote ? static_cast<unsigned>(kk >= 0 ? kk : 0) : static_cast<unsigned>(kSpecBranches)) *
                                (Spad * static_cast<unsigned>(L)) + s * L + static_cast<unsigned>(lane);
+      const unsigned ocol = static_cast<unsigned>(kSpecBranches) * (Spad * static_cast<unsigned>(L)) + s * L +
+                            static_cast<unsigned>(lane);
+      const int32_t P0 = FanShare<G>::value && AC.n == 9 ? min(max(B, sm_pbase), cur) : B;
+      auto col_of = [&](int32_t f) __attribute__((always_inline)) { return f <= P0 ? ocol : col; };
       const bool has = lane < P;
       if (F > B && ok && has) {  // the branch at F must be the cell the reference loads
         const unsigned fslot = static_cast<unsigned>(F % W);
         uint32_t bw[NW], cw[NW];
-        load_words<NW>(p.spec_cells + static_cast<size_t>(fslot) * NW * Gs, static_cast<int>(Gs), static_cast<int>(col), bw);
+        load_words<NW>(p.spec_cells + static_cast<size_t>(fslot) * NW * Gs, static_cast<int>(Gs), static_cast<int>(col_of(F)), bw);
         if constexpr (kLdsC) {
 #pragma unroll
           for (int n = 0; n < NW; ++n) cw[n] = lds_cell[(fslot * NW + n) * bd + tid];
@@ -1204,7 +1217,7 @@ p2p_kernel(const P2PParams p) {
       for (int32_t f = F + 1; f < cur; ++f) {  // the cells adjust would have saved
         const unsigned slot = static_cast<unsigned>(f % W);
         uint32_t cw[NW] = {};
-        if (has) load_words<NW>(p.spec_cells + static_cast<size_t>(slot) * NW * Gs, static_cast<int>(Gs), static_cast<int>(col), cw);
+        if (has) load_words<NW>(p.spec_cells + static_cast<size_t>(slot) * NW * Gs, static_cast<int>(Gs), static_cast<int>(col_of(f)), cw);
         if (has) {
           if constexpr (kLdsC) {
 #pragma unroll
@@ -1935,15 +1948,82 @@ p2p_kernel(const P2PParams p) {
         for (int b = 0; b < NG; ++b)
           if (on[b]) store_words<NW>(p.spec_state, static_cast<int>(Gs), static_cast<int>(col[b]), wb[b]);
       };
-      int ns = 0;  // the chain slots the wave runs: the most any of its lanes needs
+      if constexpr (FanShare<G>::value && nb == 9) {
+        // A remote player's classes agree until its first unconfirmed frame pb: the frames up to it
+        // are run once, their cells stored in the lane's own column (the one a local player's chain
+        // uses; select_per_player reads frames up to P0 there).  From P0 on the nine classes are
+        // three turn groups (no turn, left, right) of three thrusts each: per group and frame one
+        // rotation step and one sine / cosine serve its three classes (ExGame::fan_turn / fan_thrust,
+        // fan_move per class), where every class ran the whole AdvanceFrame before.
+        if (my_remote) {
+          const int32_t P0 = min(max(B, sm_pbase), cur);
+          uint32_t x[NW];
 #pragma unroll
-      for (int sb = 0; sb < kSpecBranches; ++sb) ns += __any(sb < nsl) ? 1 : 0;
-      for (int b0 = 0; b0 < ns; b0 += kFanGroup) {
-        const int ng = min(kFanGroup, ns - b0);
-        if (ng == 1) group(std::integral_constant<int, 1>{}, b0);
-        else if (ng == 2 || kFanGroup == 2) group(std::integral_constant<int, 2>{}, b0);
-        else if (ng == 3 || kFanGroup == 3) group(std::integral_constant<int, 3>{}, b0);
-        else group(std::integral_constant<int, (kFanGroup >= 4 ? 4 : 3)>{}, b0);
+          for (int n = 0; n < NW; ++n) x[n] = ow[n];
+          unsigned fsl = bslot;
+          for (int32_t f = B; f < P0; ++f, fsl = fsl + 1 == static_cast<unsigned>(W) ? 0u : fsl + 1) {
+            if (f > B && !(RB_FAN_EXP & 2))
+              store_words<NW>(p.spec_cells + static_cast<size_t>(fsl) * NW * Gs, static_cast<int>(Gs), static_cast<int>(ocol), x);
+            const int j = f - B;
+            const uint32_t v = j < kFanPre ? fan_input(vpk, j) : ring.get(f, h_own, s);  // confirmed (f <= la_own)
+            adv(x, static_cast<InRec>(static_cast<uint64_t>(v) << (8 * h_own)));
+          }
+          if (P0 > B && P0 < cur && !(RB_FAN_EXP & 2))  // the cell of frame P0, common to every class
+            store_words<NW>(p.spec_cells + static_cast<size_t>(fsl) * NW * Gs, static_cast<int>(Gs), static_cast<int>(ocol), x);
+          constexpr auto ACs = AlphabetClasses<G>::value;
+          constexpr uint32_t kSlots = static_cast<uint32_t>(class_slot(ACs, 0)) | static_cast<uint32_t>(class_slot(ACs, 1)) << 4 |
+                                      static_cast<uint32_t>(class_slot(ACs, 2)) << 8 | static_cast<uint32_t>(class_slot(ACs, 4)) << 12 |
+                                      static_cast<uint32_t>(class_slot(ACs, 5)) << 16 | static_cast<uint32_t>(class_slot(ACs, 6)) << 20 |
+                                      static_cast<uint32_t>(class_slot(ACs, 8)) << 24 | static_cast<uint32_t>(class_slot(ACs, 9)) << 28;
+          constexpr uint32_t kSlot10 = static_cast<uint32_t>(class_slot(ACs, 10));
+#pragma unroll 1
+          for (int tg = 0; tg < 3; ++tg) {  // turn groups: class bits 2-3 = 0, 4 (left), 8 (right); one at a time
+            const uint32_t turn = static_cast<uint32_t>(tg) * 4u;
+            uint32_t wb[3][NW];
+            unsigned cc[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {  // thrust: class bits 0-1 = 0, 1 (up), 2 (down)
+              const int q = tg * 3 + c;  // the class slots of (turn, thrust) in the AlphabetClasses order
+              cc[c] = q < 8 ? (kSlots >> (4 * q)) & 15u : kSlot10;
+#pragma unroll
+              for (int n = 0; n < NW; ++n) wb[c][n] = x[n];
+            }
+            float rot = __uint_as_float(x[4]);
+            SinCos th{0.0f, 0.0f};
+            if (tg == 0) th = inr ? G::template fan_thrust<true>(rot, &p.counters[1]) : G::template fan_thrust<false>(rot, &p.counters[1]);
+            unsigned fs2 = fsl;
+            for (int32_t f = P0; f < cur; ++f, fs2 = fs2 + 1 == static_cast<unsigned>(W) ? 0u : fs2 + 1) {
+              if (f > P0 && !(RB_FAN_EXP & 2)) {
+#pragma unroll
+                for (int c = 0; c < 3; ++c)
+                  store_words<NW>(p.spec_cells + static_cast<size_t>(fs2) * NW * Gs, static_cast<int>(Gs),
+                                  static_cast<int>(cc[c] * (Spad * static_cast<unsigned>(L)) + bcol), wb[c]);
+              }
+              if (tg != 0) th = inr ? G::template fan_thrust<true>(rot, &p.counters[1]) : G::template fan_thrust<false>(rot, &p.counters[1]);
+#pragma unroll
+              for (int c = 0; c < 3; ++c) G::fan_move(wb[c], th.c, th.s, static_cast<uint32_t>(c));
+              rot = inr ? G::template fan_turn<true>(rot, turn) : G::template fan_turn<false>(rot, turn);
+#pragma unroll
+              for (int c = 0; c < 3; ++c) wb[c][4] = __float_as_uint(rot);
+            }
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+              store_words<NW>(p.spec_state, static_cast<int>(Gs), static_cast<int>(cc[c] * (Spad * static_cast<unsigned>(L)) + bcol), wb[c]);
+          }
+        } else if (lane < P) {
+          group(std::integral_constant<int, 1>{}, 0);  // a local player's one chain
+        }
+      } else {
+        int ns = 0;  // the chain slots the wave runs: the most any of its lanes needs
+#pragma unroll
+        for (int sb = 0; sb < kSpecBranches; ++sb) ns += __any(sb < nsl) ? 1 : 0;
+        for (int b0 = 0; b0 < ns; b0 += kFanGroup) {
+          const int ng = min(kFanGroup, ns - b0);
+          if (ng == 1) group(std::integral_constant<int, 1>{}, b0);
+          else if (ng == 2 || kFanGroup == 2) group(std::integral_constant<int, 2>{}, b0);
+          else if (ng == 3 || kFanGroup == 3) group(std::integral_constant<int, 3>{}, b0);
+          else group(std::integral_constant<int, (kFanGroup >= 4 ? 4 : 3)>{}, b0);
+        }
       }
       tot_branch += static_cast<uint32_t>(cur - B) * static_cast<uint32_t>(nb * nrem);
     }

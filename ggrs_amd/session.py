@@ -248,20 +248,31 @@ class SessionBuilder:
         return self
 
     def with_speculative_fanout(self, on: bool, candidates: int = 16, adaptive: bool = True,
-                                min_select_permille: int = 0, per_player: bool = False) -> "SessionBuilder":
+                                min_select_permille: int = 0, per_player=None) -> "SessionBuilder":
         """P2P: presimulate `candidates` (1..16) candidate inputs of the
         most-lagging remote handle after every tick (RB_P2P_FLAG_FANOUT,
         BASELINE config 4): the whole input alphabet when it has at most that
         many values (ex_game), else the most likely ones (include/ggrs_amd.h).
         adaptive: pause it while too few rollbacks become selects (below
         min_select_permille, 0 = the engine's default; RB_P2P_FLAG_FANOUT_ALWAYS
-        when False)."""
+        when False).  per_player: speculate every remote player
+        (RB_P2P_FLAG_FANOUT_PER_PLAYER) rather than the one with the oldest
+        unconfirmed input; None (default) = per player where the game's players
+        move independently and the candidates cover its input alphabet
+        (ex_game at 16: 66% of C4's rollbacks become selects instead of 31%)."""
         self._fanout = bool(on)
         self._fanout_k = int(candidates)
         self._fanout_adaptive = bool(adaptive)
         self._fanout_permille = int(min_select_permille)
-        self._fanout_per_player = bool(per_player)  # RB_P2P_FLAG_FANOUT_PER_PLAYER: every remote player
+        self._fanout_per_player = per_player  # RB_P2P_FLAG_FANOUT_PER_PLAYER: every remote player (None: start decides)
         return self
+
+    def _per_player_resolved(self) -> bool:
+        pp = getattr(self, "_fanout_per_player", False)
+        if pp is None:  # the games whose players move independently (games.hpp kIndependentPlayers)
+            pp = (self._cfg.game == Game.EX_GAME and int(self._cfg.num_players) >= 2
+                  and getattr(self, "_fanout_k", 16) >= 16)
+        return bool(pp) and getattr(self, "_fanout", False)
 
     def with_desync_detection_mode(self, interval: int) -> "SessionBuilder":  # builder.rs:169-172
         """P2P: DesyncDetection::On{interval} for interval > 0, Off for 0 (default)."""
@@ -307,7 +318,7 @@ class SessionBuilder:
         pc.flags = (self._cfg.flags & L.RB_FLAG_LANE_PER_SESSION) | (
             L.RB_P2P_FLAG_FANOUT if getattr(self, "_fanout", False) else 0) | (
             L.RB_P2P_FLAG_FANOUT_ALWAYS if not getattr(self, "_fanout_adaptive", True) else 0) | (
-            L.RB_P2P_FLAG_FANOUT_PER_PLAYER if getattr(self, "_fanout_per_player", False) else 0) | (
+            L.RB_P2P_FLAG_FANOUT_PER_PLAYER if self._per_player_resolved() else 0) | (
             L.RB_P2P_FLAG_PEER_STATUS if getattr(self, "_peer_status", False) else 0)
         pc.block_size = self._cfg.block_size
         pc.desync_interval = getattr(self, "_desync", 0)

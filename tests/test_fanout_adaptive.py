@@ -14,6 +14,7 @@ W, D, RD = 8, 2, 2
 
 
 def batch(game, P, S, fanout, **kw):
+    kw.setdefault("per_player", False)  # the one-player form (the default for ex_game is per player)
     b = (G.SessionBuilder(game, num_sessions=S).with_num_players(P).with_max_prediction_window(W)
          .with_input_delay(D).with_remote_input_delay(RD).with_speculative_fanout(fanout, 16, **kw))
     for h in range(P):
@@ -132,3 +133,22 @@ def test_gpu_brawler_fanout_branch_slots_above_4g_words(gpu_available):
     assert tf[2] + tf[3] == tp[2]
     fan.close()
     plain.close()
+
+
+def test_gpu_default_fanout_is_per_player_for_ex_game(gpu_available):
+    """with_speculative_fanout's default for a game whose players move independently (ex_game, K
+    covering its alphabet) is the per-player form; it equals plain rollback and selects more
+    rollbacks than the one-player form on the same inputs."""
+    import torch
+    P, S, T, tpl = 4, 256, 120, 20
+    inputs, upto, rin = synth_network(S, P, T, 0b1, RD, 1, 4)
+    di, du, dr = (torch.from_numpy(a).cuda() for a in (inputs, upto, rin))
+    auto = batch(G.Game.EX_GAME, P, S, True, per_player=None, adaptive=False)
+    one = batch(G.Game.EX_GAME, P, S, True, adaptive=False)
+    plain = batch(G.Game.EX_GAME, P, S, False)
+    drive([auto, one, plain], di, du, dr, T, tpl)
+    same(auto, plain)
+    same(one, plain)
+    ta, to, tp = auto.totals(), one.totals(), plain.totals()
+    assert ta[2] + ta[3] == tp[2] and to[2] + to[3] == tp[2]
+    assert ta[3] > to[3] > 0, (ta, to)  # selects: per player > one player

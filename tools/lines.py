@@ -66,11 +66,12 @@ LINES = {
                     f"{QB} S=65536", 50),
     "brawler_p2p_sparse": (f"--game brawler {P2P} --sparse-saving --steps 100 --warmup 50",
                            f"--game brawler {P2P} --sparse-saving --steps 100 --warmup 50", f"{QB} S=65536 sparse", 50),
+    # config 4: the default fan-out (per player for ex_game at K = 16), and the one-player form
     "c4": (f"{P2P} --num-players 4 --fanout --steps 100 --warmup 50", f"{P2P} --num-players 4 --fanout --steps 100 --warmup 50",
-           f"{Q4} S=65536 fanout", 50),
-    "c4_pp": (f"{P2P} --num-players 4 --fanout --fanout-mode per-player --steps 100 --warmup 50",
-              f"{P2P} --num-players 4 --fanout --fanout-mode per-player --steps 100 --warmup 50",
-              f"{Q4} S=65536 fanout per-player", 50),
+           f"{Q4} S=65536 fanout per-player", 50),
+    "c4_one": (f"{P2P} --num-players 4 --fanout --fanout-mode single --steps 100 --warmup 50",
+               f"{P2P} --num-players 4 --fanout --fanout-mode single --steps 100 --warmup 50",
+               f"{Q4} S=65536 fanout", 50),
     "c4_k8": (f"{P2P} --num-players 4 --fanout --fanout-k 8 --steps 100 --warmup 50",
               f"{P2P} --num-players 4 --fanout --fanout-k 8 --steps 100 --warmup 50", f"{Q4} S=65536 fanout8", 50),
     "brawler_fan": (f"--game brawler {P2P} --fanout --steps 20 --warmup 100 --ticks-per-launch 20",
