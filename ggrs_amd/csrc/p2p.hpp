@@ -34,33 +34,89 @@
 
 namespace rb {
 
-// Per-session scalar rows of P2PParams::qs.
+// The persistent bookkeeping of a P2P session (P2PParams::qs, [kQsFields][Spad] i32), packed: every
+// frame number is a 16-bit delta from the session's current frame (fd_enc), so a one-tick launch
+// reads and writes 4 words per player instead of 9 and 8 (the bookkeeping was
+// 6.2x the tick's algorithmic bytes).  The deltas a session can hold are bounded by the input queue
+// (128 frames) and the prediction window, except a disconnected player's frozen frames and extreme
+// deliveries: a value outside the 16-bit range sets the row's escape code and is kept in absolute
+// rows, written and read only then, so every value stays exact.
 enum : int {
   QS_CUR = 0,         // SyncLayer::current_frame
-  QS_LAST_SAVED = 1,  // SyncLayer::last_saved_frame
-  QS_LAST_CONF = 2,   // SyncLayer::last_confirmed_frame
-  QS_DISC_FRAME = 3,  // P2PSession::disconnect_frame (p2p_session.rs:130)
-  QS_PLAYER0 = 4,     // + field * 4 + player (4 player slots)
+  QS_SAVED_CONF = 1,  // SyncLayer::last_saved_frame | last_confirmed_frame << 16 (deltas; kQsEscWord: absolute rows)
+  QS_DISC_FRAME = 2,  // P2PSession::disconnect_frame (p2p_session.rs:130), stored only when it changes
+  QS_ABS_SAVED = 3,   // the absolute frames behind kQsEscWord
+  QS_ABS_CONF = 4,
+  QS_PLAYER0 = 5,     // + field * 4 + player (4 player slots)
 };
 enum : int {
-  QF_LAST_ADDED = 0,   // InputQueue::last_added_frame
-  QF_PRED_FRAME = 1,   // InputQueue::prediction.frame
-  QF_PRED_VAL = 2,     // InputQueue::prediction.input
-  QF_FIRST_INC = 3,    // InputQueue::first_incorrect_frame
-  QF_LAST_REQ = 4,     // InputQueue::last_requested_frame
-  QF_CONN_LAST = 5,    // ConnectionStatus::last_frame (messages.rs:5-18)
-  QF_DISC = 6,         // ConnectionStatus::disconnected (0 / 1)
-  QF_TAIL = 7,         // InputQueue: frame of inputs[tail] (input_queue.rs:83-101)
-  QF_LEN = 8,          // InputQueue::length
+  QF_LA_CONN = 0,   // InputQueue::last_added_frame | ConnectionStatus::last_frame << 16 (messages.rs:5-18), deltas
+  QF_PRED_FI = 1,   // InputQueue::prediction.frame | first_incorrect_frame << 16, deltas
+  QF_REQ_TAIL = 2,  // InputQueue::last_requested_frame | frame of inputs[tail] << 16 (input_queue.rs:83-101), deltas
+  QF_MISC = 3,      // InputQueue::length (i16) | disconnected << 16 | escape << 17 | prediction.input << 24 (1-byte inputs)
+  QF_PRED_VAL = 4,  // InputQueue::prediction.input of inputs wider than a byte
+  QF_ABS0 = 5,      // 7 rows behind the escape bit: last added, connection, prediction, first incorrect, requested, tail, length
   // the fan-out's candidate list (not GGRS state): the queue's 16 most recent distinct
   // inputs, newest first, as two u64 (4 rows), and their count
-  QF_MTF0 = 9,
-  QF_MTF_N = 13,
-  QF_COUNT = 14,
+  QF_MTF0 = 12,
+  QF_MTF_N = 16,
+  QF_COUNT = 17,
 };
 constexpr int kQsFields = QS_PLAYER0 + QF_COUNT * 4;
-// trace rows (the last tick of the last launch): LoadGameState frame, AdvanceFrame count, SaveGameState count
-enum : int { TR_LOAD = 0, TR_NADV = 1, TR_NSAVE = 2, TR_COUNT = 3 };
+constexpr uint32_t kFdNull = 0x8000u, kFdEsc = 0x8001u;  // 16-bit codes: NULL_FRAME, escaped
+constexpr uint32_t kQsEscWord = kFdEsc | kFdEsc << 16;
+constexpr uint32_t kQmDisc = 1u << 16, kQmEsc = 1u << 17;
+__host__ __device__ __forceinline__ bool fd_fits(int32_t f, int32_t base) {
+  return f == kNullFrame || (f - base >= -32766 && f - base <= 32767);
+}
+__host__ __device__ __forceinline__ uint32_t fd_enc(int32_t f, int32_t base) {
+  return f == kNullFrame ? kFdNull : static_cast<uint32_t>(f - base) & 0xFFFFu;
+}
+__host__ __device__ __forceinline__ int32_t fd_dec(uint32_t v, int32_t base) {
+  v &= 0xFFFFu;
+  return v == kFdNull ? kNullFrame : base + static_cast<int32_t>(static_cast<int16_t>(static_cast<uint16_t>(v)));
+}
+// One player's queue fields and their packed rows QF_LA_CONN .. QF_MISC (esc: the absolute rows hold them)
+struct QFields {
+  int32_t la, conn, pred, fi, req, tail, len;
+  bool disc;
+  uint32_t pv;  // prediction.input (the QF_MISC byte for 1-byte inputs)
+};
+struct QPacked {
+  uint32_t w[4];
+  bool esc;
+};
+__host__ __device__ __forceinline__ QPacked q_pack(const QFields& f, int32_t cur) {
+  const bool esc = !(fd_fits(f.la, cur) && fd_fits(f.conn, cur) && fd_fits(f.pred, cur) && fd_fits(f.fi, cur) &&
+                     fd_fits(f.req, cur) && fd_fits(f.tail, cur) && f.len >= -32768 && f.len <= 32767);
+  QPacked r;
+  r.w[0] = fd_enc(f.la, cur) | fd_enc(f.conn, cur) << 16;
+  r.w[1] = fd_enc(f.pred, cur) | fd_enc(f.fi, cur) << 16;
+  r.w[2] = fd_enc(f.req, cur) | fd_enc(f.tail, cur) << 16;
+  r.w[3] = (static_cast<uint32_t>(f.len) & 0xFFFFu) | (f.disc ? kQmDisc : 0u) | (esc ? kQmEsc : 0u) | (f.pv & 0xFFu) << 24;
+  r.esc = esc;
+  return r;
+}
+// abs: the 7 absolute rows (read only when the escape bit is set)
+__host__ __device__ __forceinline__ QFields q_unpack(const uint32_t (&w)[4], int32_t cur, const int32_t (&abs)[7]) {
+  QFields f;
+  const bool esc = (w[3] & kQmEsc) != 0;
+  f.la = esc ? abs[0] : fd_dec(w[0], cur);
+  f.conn = esc ? abs[1] : fd_dec(w[0] >> 16, cur);
+  f.pred = esc ? abs[2] : fd_dec(w[1], cur);
+  f.fi = esc ? abs[3] : fd_dec(w[1] >> 16, cur);
+  f.req = esc ? abs[4] : fd_dec(w[2], cur);
+  f.tail = esc ? abs[5] : fd_dec(w[2] >> 16, cur);
+  f.len = esc ? abs[6] : static_cast<int32_t>(static_cast<int16_t>(static_cast<uint16_t>(w[3] & 0xFFFFu)));
+  f.disc = (w[3] & kQmDisc) != 0;
+  f.pv = w[3] >> 24;
+  return f;
+}
+// trace word (the last tick of the last launch): LoadGameState frame as a delta from the current
+// frame | AdvanceFrame count << 16 | SaveGameState count << 24 (at most 2 * 64 + 1 each; 0xFF: none yet)
+__host__ __device__ __forceinline__ uint32_t trace_pack(int32_t load_frame, int32_t nadv, int32_t nsave, int32_t cur) {
+  return fd_enc(load_frame, cur) | (static_cast<uint32_t>(nadv) & 0xFFu) << 16 | (static_cast<uint32_t>(nsave) & 0xFFu) << 24;
+}
 constexpr int32_t kP2PStatusOk = 0, kP2PStatusThreshold = 1, kP2PStatusPanic = 101;
 // decode status of a packet-fed tick's endpoint (the codes of wire.hip's rb_decode_input_packets):
 // inputs added, nothing new, malformed (the reference panics, protocol.rs:656; also a length past
@@ -320,7 +376,7 @@ struct P2PParams {
   uint32_t* live;
   int32_t* qs;
   int32_t* status;          // [Spad] rb_status of the session's last advance_frame
-  int32_t* trace;           // [TR_COUNT][Spad]
+  int32_t* trace;           // [Spad] trace_pack words
   uint32_t* counters;       // [0] threshold hits, [1] unexpected-path count, [2] panics
   // work counters [ST_COUNT][Spad]: a wave's sum at its first session's column (or per session,
   // see the end of p2p_kernel); only their sums are read
@@ -844,7 +900,8 @@ p2p_kernel(const P2PParams p) {
   // state, cells and queues stay as the panic left them.  (Checked once the
   // session's state loads are issued, so they do not wait for this one.)
   if constexpr (RB_P2P_EXP & 32) return;  // (attribution builds only: the launch floor)
-  const bool panicked = p.status[s] == kP2PStatusPanic;
+  const int32_t status0 = p.status[s];  // (stored back only when the tick changes it)
+  const bool panicked = status0 == kP2PStatusPanic;
   const unsigned Spad = static_cast<unsigned>(p.Spad), Gpad = Spad * L;
   const unsigned slot_words = static_cast<unsigned>(NW) * Gpad;
   const int W = p.W;
@@ -876,22 +933,18 @@ p2p_kernel(const P2PParams p) {
   // cur % W, kept alongside cur (every SaveGameState is of the current frame):
   // a division by the runtime W costs a dozen VALU instructions
   unsigned cur_slot = static_cast<unsigned>(cur % p.W);
-  int32_t last_saved = p.qs[QS_LAST_SAVED * Spad + s];
-  int32_t last_conf = p.qs[QS_LAST_CONF * Spad + s];
+  // the packed bookkeeping (decoded below, once every load of the launch's entry is issued)
+  const uint32_t sc_pk = static_cast<uint32_t>(p.qs[QS_SAVED_CONF * Spad + s]);
+  int32_t last_saved = kNullFrame, last_conf = kNullFrame;
   DevQueue q[PPL];
+  uint32_t qpk[PPL][4];
 #pragma unroll
   for (int j = 0; j < PPL; ++j) {
     const int h = player_of(j);
     if (h < P) {
-      q[j].last_added = *qrow(QF_LAST_ADDED, h);
-      q[j].pred_frame = *qrow(QF_PRED_FRAME, h);
-      q[j].pred_val = static_cast<uint32_t>(*qrow(QF_PRED_VAL, h));
-      q[j].first_inc = *qrow(QF_FIRST_INC, h);
-      q[j].last_req = *qrow(QF_LAST_REQ, h);
-      q[j].conn_last = *qrow(QF_CONN_LAST, h);
-      q[j].disc = *qrow(QF_DISC, h) != 0;
-      q[j].tail = *qrow(QF_TAIL, h);
-      q[j].len = *qrow(QF_LEN, h);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) qpk[j][i] = static_cast<uint32_t>(*qrow(QF_LA_CONN + i, h));
+      if constexpr (IB > 1) q[j].pred_val = static_cast<uint32_t>(*qrow(QF_PRED_VAL, h));
       q[j].bad = false;
       // the fan-out's candidate list, for an alphabet larger than K
       q[j].mtf = kSpec && kMtf;
@@ -903,15 +956,15 @@ p2p_kernel(const P2PParams p) {
       }
     } else {  // padding lane of a 4-lane group (P = 3): no player
       q[j] = DevQueue{kNullFrame, kNullFrame, kNullFrame, kNullFrame, INT32_MAX, 0u, false, 0};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) qpk[j][i] = 0u;
     }
   }
   // disconnect_player between launches: P2PSession::disconnect_frame, consumed
   // by the next advance_frame's check_simulation_consistency (:281-288)
   int32_t disc_frame = p.qs[QS_DISC_FRAME * Spad + s];
-  bool any_disc = false;
-#pragma unroll
-  for (int j = 0; j < PPL; ++j) any_disc |= q[j].disc;
-  any_disc = group_min<L>(any_disc ? 0 : 1) == 0;
+  const int32_t disc_frame0 = disc_frame;
+  bool any_disc = false;  // (after the decode below)
   // confirmed_frame (:487-498) skips disconnected players
   auto conn_of = [&](int j) __attribute__((always_inline)) { return q[j].disc ? INT32_MAX : q[j].conn_last; };
   uint32_t w[NW];
@@ -999,6 +1052,38 @@ p2p_kernel(const P2PParams p) {
 #pragma unroll
     for (int j = 0; j < PPL; ++j) pre0[j] = wire_fetch(min(player_of(j), P - 1), 0);
   }
+  // ---- the packed bookkeeping decoded (q_unpack); a row with a value past its 16-bit deltas reads
+  // its absolute rows (a branch taken only then, after every entry load above is in flight)
+  if (sc_pk == kQsEscWord) {
+    last_saved = p.qs[QS_ABS_SAVED * Spad + s];
+    last_conf = p.qs[QS_ABS_CONF * Spad + s];
+  } else {
+    last_saved = fd_dec(sc_pk, cur);
+    last_conf = fd_dec(sc_pk >> 16, cur);
+  }
+#pragma unroll
+  for (int j = 0; j < PPL; ++j) {
+    const int h = player_of(j);
+    if (h >= P) continue;
+    int32_t ab[7] = {0, 0, 0, 0, 0, 0, 0};
+    if (qpk[j][3] & kQmEsc) {
+#pragma unroll
+      for (int i = 0; i < 7; ++i) ab[i] = *qrow(QF_ABS0 + i, h);
+    }
+    const QFields f = q_unpack(qpk[j], cur, ab);
+    q[j].last_added = f.la;
+    q[j].conn_last = f.conn;
+    q[j].pred_frame = f.pred;
+    q[j].first_inc = f.fi;
+    q[j].last_req = f.req;
+    q[j].tail = f.tail;
+    q[j].len = f.len;
+    q[j].disc = f.disc;
+    if constexpr (IB == 1) q[j].pred_val = f.pv;
+  }
+#pragma unroll
+  for (int j = 0; j < PPL; ++j) any_disc |= q[j].disc;
+  any_disc = group_min<L>(any_disc ? 0 : 1) == 0;
   if (panicked) return;
 #if RB_P2P_PHASE
   settle(static_cast<uint32_t>(cur));
@@ -2351,15 +2436,17 @@ p2p_kernel(const P2PParams p) {
   for (int j = 0; j < PPL; ++j) {
     const int h = player_of(j);
     if (h >= P) continue;
-    *qrow(QF_LAST_ADDED, h) = q[j].last_added;
-    *qrow(QF_PRED_FRAME, h) = q[j].pred_frame;
-    *qrow(QF_PRED_VAL, h) = static_cast<int32_t>(q[j].pred_val);
-    *qrow(QF_FIRST_INC, h) = q[j].first_inc;
-    *qrow(QF_LAST_REQ, h) = q[j].last_req;
-    *qrow(QF_CONN_LAST, h) = q[j].conn_last;
-    *qrow(QF_TAIL, h) = q[j].tail;
-    *qrow(QF_LEN, h) = q[j].len;
-    if constexpr (kNet) *qrow(QF_DISC, h) = q[j].disc ? 1 : 0;  // update_player_disconnects may set it
+    const QFields f{q[j].last_added, q[j].conn_last, q[j].pred_frame, q[j].first_inc, q[j].last_req,
+                    q[j].tail,       q[j].len,       q[j].disc,       q[j].pred_val};
+    const QPacked pk = q_pack(f, cur);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *qrow(QF_LA_CONN + i, h) = static_cast<int32_t>(pk.w[i]);
+    if constexpr (IB > 1) *qrow(QF_PRED_VAL, h) = static_cast<int32_t>(q[j].pred_val);
+    if (pk.esc) {
+      const int32_t ab[7] = {f.la, f.conn, f.pred, f.fi, f.req, f.tail, f.len};
+#pragma unroll
+      for (int i = 0; i < 7; ++i) *qrow(QF_ABS0 + i, h) = ab[i];
+    }
     if constexpr (kSpec && kMtf) {
       {
         *qrow(QF_MTF0, h) = static_cast<int32_t>(q[j].mlo);
@@ -2414,16 +2501,18 @@ p2p_kernel(const P2PParams p) {
   }
   if (lead) {
     p.qs[QS_CUR * Spad + s] = cur;
-    p.qs[QS_LAST_SAVED * Spad + s] = last_saved;
-    p.qs[QS_LAST_CONF * Spad + s] = last_conf;
-    p.qs[QS_DISC_FRAME * Spad + s] = disc_frame;
-    p.status[s] = status;
+    const bool sesc = !(fd_fits(last_saved, cur) && fd_fits(last_conf, cur));
+    p.qs[QS_SAVED_CONF * Spad + s] = static_cast<int32_t>(sesc ? kQsEscWord : fd_enc(last_saved, cur) | fd_enc(last_conf, cur) << 16);
+    if (sesc) {
+      p.qs[QS_ABS_SAVED * Spad + s] = last_saved;
+      p.qs[QS_ABS_CONF * Spad + s] = last_conf;
+    }
+    if (disc_frame != disc_frame0) p.qs[QS_DISC_FRAME * Spad + s] = disc_frame;
+    if (status != status0) p.status[s] = status;
     if (status == kP2PStatusPanic) atomicAdd(&p.counters[2], 1u);
     if (n_thr) atomicAdd(&p.counters[0], n_thr);
     if constexpr (!(RB_P2P_EXP & 64)) {  // (attribution builds: 64 drops the trace and work-counter traffic)
-      p.trace[TR_LOAD * Spad + s] = load_frame;
-      p.trace[TR_NADV * Spad + s] = nadv;
-      p.trace[TR_NSAVE * Spad + s] = nsave;
+      p.trace[s] = static_cast<int32_t>(trace_pack(load_frame, nadv, nsave, cur));
       if (!wave_summed) {
         atomicAdd(&p.stats[ST_ADV * Spad + s], static_cast<unsigned long long>(tot_adv));
         atomicAdd(&p.stats[ST_SAVE * Spad + s], static_cast<unsigned long long>(tot_save));
@@ -2517,13 +2606,17 @@ __global__ void __launch_bounds__(256) fanout_kernel(const FanParams p) {
   const RingIO<IB> ring{const_cast<uint8_t*>(reinterpret_cast<const uint8_t*>(p.ring)), P, p.Spad};
   auto qrow = [&](int field, int h) { return p.qs[static_cast<size_t>(QS_PLAYER0 + field * 4 + h) * Spad + s]; };
   const int32_t cur = p.qs[QS_CUR * Spad + s];
+  auto last_added_of = [&](int h) {  // InputQueue::last_added_frame from the packed rows (q_unpack)
+    const uint32_t m = static_cast<uint32_t>(qrow(QF_MISC, h));
+    return (m & kQmEsc) ? qrow(QF_ABS0, h) : fd_dec(static_cast<uint32_t>(qrow(QF_LA_CONN, h)), cur);
+  };
   // the remote handle with the oldest last added input (ties: lowest handle)
   int rs = -1;
   int32_t la_rs = INT32_MAX;
 #pragma unroll
   for (int h = 0; h < P; ++h) {
     if ((p.local_mask >> h) & 1u) continue;
-    const int32_t la = qrow(QF_LAST_ADDED, h);
+    const int32_t la = last_added_of(h);
     const int32_t key = la == kNullFrame ? -1 : la;
     if (key < la_rs) {
       la_rs = key;
@@ -2532,7 +2625,7 @@ __global__ void __launch_bounds__(256) fanout_kernel(const FanParams p) {
   }
   bool any_disc = false;
 #pragma unroll
-  for (int h = 0; h < P; ++h) any_disc |= qrow(QF_DISC, h) != 0;
+  for (int h = 0; h < P; ++h) any_disc |= (static_cast<uint32_t>(qrow(QF_MISC, h)) & kQmDisc) != 0;
   const int32_t base = la_rs + 1;  // first unconfirmed frame of the speculated player
   const bool valid = p.status[s] != kP2PStatusPanic && !any_disc && rs >= 0 && base < cur && base + W > cur && base >= 0 &&
                      p.tag[static_cast<unsigned>(base % W) * Spad + s] == base;
@@ -2563,7 +2656,7 @@ __global__ void __launch_bounds__(256) fanout_kernel(const FanParams p) {
   const int h = lane;
   const bool active = h < P;
   const bool local = active && ((p.local_mask >> h) & 1u);
-  const int32_t la_h = active ? qrow(QF_LAST_ADDED, h) : kNullFrame;
+  const int32_t la_h = active ? last_added_of(h) : kNullFrame;
   const uint32_t pred = (!active || la_h == kNullFrame) ? 0u : ring.get(la_h, h, s);
   uint32_t vin[kFanPre];
   fan_prefetch(ring, active ? h : 0, s, base, cur, local, la_h, pred, vin);

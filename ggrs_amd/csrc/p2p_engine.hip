@@ -135,9 +135,12 @@ __global__ void p2p_disconnect_kernel(int32_t* qs, const uint8_t* mask, int32_t 
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= S || (mask && !mask[s])) return;
   const size_t sp = static_cast<size_t>(Spad);
-  const int32_t last = qs[(QS_PLAYER0 + QF_CONN_LAST * 4 + h) * sp + s];
-  qs[(QS_PLAYER0 + QF_DISC * 4 + h) * sp + s] = 1;
-  if (qs[QS_CUR * sp + s] > last) qs[QS_DISC_FRAME * sp + s] = last + 1;
+  auto row = [&](int field) -> int32_t& { return qs[(QS_PLAYER0 + field * 4 + h) * sp + s]; };
+  const int32_t cur = qs[QS_CUR * sp + s];
+  const uint32_t m = static_cast<uint32_t>(row(QF_MISC));
+  const int32_t last = (m & kQmEsc) ? row(QF_ABS0 + 1) : fd_dec(static_cast<uint32_t>(row(QF_LA_CONN)) >> 16, cur);
+  row(QF_MISC) = static_cast<int32_t>(m | kQmDisc);
+  if (cur > last) qs[QS_DISC_FRAME * sp + s] = last + 1;
 }
 
 // UdpProtocol::on_checksum_report (protocol.rs:710-722) for the endpoint of
@@ -316,7 +319,7 @@ rb_status rb_p2p_create(const rb_p2p_config* cfg, rb_p2p** out) {
   P2P_CREATE(hipMalloc(&b->live, NW * Gp * 4));
   P2P_CREATE(hipMalloc(&b->qs, kQsFields * Sp * 4));
   P2P_CREATE(hipMalloc(&b->status, Sp * 4));
-  P2P_CREATE(hipMalloc(&b->trace, TR_COUNT * Sp * 4));
+  P2P_CREATE(hipMalloc(&b->trace, Sp * 4));
   P2P_CREATE(hipMalloc(&b->counters, 16));
   P2P_CREATE(hipMalloc(&b->stats, ST_COUNT * Sp * 8));
   P2P_CREATE(hipMemsetAsync(b->snap, 0, W * NW * Gp * 4, b->stream));
@@ -324,7 +327,7 @@ rb_status rb_p2p_create(const rb_p2p_config* cfg, rb_p2p** out) {
   P2P_CREATE(hipMemsetAsync(b->tag, 0xff, W * Sp * 4, b->stream));  // GameState::default frame = NULL_FRAME
   P2P_CREATE(hipMemsetAsync(b->ring, 0, ring_bytes, b->stream));     // blank inputs
   P2P_CREATE(hipMemsetAsync(b->status, 0, Sp * 4, b->stream));
-  P2P_CREATE(hipMemsetAsync(b->trace, 0xff, TR_COUNT * Sp * 4, b->stream));
+  P2P_CREATE(hipMemsetAsync(b->trace, 0xff, Sp * 4, b->stream));  // no tick yet: NULL load frame (at frame 0), counts 0xFF
   P2P_CREATE(hipMemsetAsync(b->counters, 0, 16, b->stream));
   P2P_CREATE(hipMemsetAsync(b->stats, 0, ST_COUNT * Sp * 8, b->stream));
   if (b->fanout) {
@@ -344,15 +347,16 @@ rb_status rb_p2p_create(const rb_p2p_config* cfg, rb_p2p** out) {
       P2P_CREATE(hipEventCreateWithFlags(&b->fan.ev, hipEventDisableTiming));
     }
   }
-  // SyncLayer::new / InputQueue::new / ConnectionStatus::default: every frame NULL, current 0
+  // SyncLayer::new / InputQueue::new / ConnectionStatus::default: every frame NULL, current 0,
+  // connected, length 0, the first input at frame 0 (q_pack)
   std::vector<int32_t> qs(kQsFields * Sp, kNullFrame);
+  const QPacked q0 = q_pack(QFields{kNullFrame, kNullFrame, kNullFrame, kNullFrame, kNullFrame, 0, 0, false, 0u}, 0);
   for (size_t s = 0; s < Sp; ++s) {
     qs[QS_CUR * Sp + s] = 0;
+    qs[QS_SAVED_CONF * Sp + s] = static_cast<int32_t>(fd_enc(kNullFrame, 0) | fd_enc(kNullFrame, 0) << 16);
     for (int h = 0; h < 4; ++h) {
+      for (int i = 0; i < 4; ++i) qs[(QS_PLAYER0 + (QF_LA_CONN + i) * 4 + h) * Sp + s] = static_cast<int32_t>(q0.w[i]);
       qs[(QS_PLAYER0 + QF_PRED_VAL * 4 + h) * Sp + s] = 0;
-      qs[(QS_PLAYER0 + QF_DISC * 4 + h) * Sp + s] = 0;  // ConnectionStatus::default: connected
-      qs[(QS_PLAYER0 + QF_TAIL * 4 + h) * Sp + s] = 0;  // every queue's first input is frame 0
-      qs[(QS_PLAYER0 + QF_LEN * 4 + h) * Sp + s] = 0;
       qs[(QS_PLAYER0 + QF_MTF_N * 4 + h) * Sp + s] = 0;  // the fan-out's candidate list starts empty
     }
   }
@@ -695,7 +699,7 @@ rb_status rb_p2p_disconnect_player(rb_p2p* b, int32_t handle, const uint8_t* ses
     if (r != RB_OK) return r;
     for (int h = 0; h < b->P; ++h)
       for (int s = 0; s < b->S; ++s)
-        b->disconnected[static_cast<size_t>(h) * b->S + s] = qs[(QS_PLAYER0 + QF_DISC * 4 + h) * b->Spad + s] != 0;
+        b->disconnected[static_cast<size_t>(h) * b->S + s] = (static_cast<uint32_t>(qs[(QS_PLAYER0 + QF_MISC * 4 + h) * b->Spad + s]) & kQmDisc) != 0;
   }
   uint8_t* d = b->disconnected.data() + static_cast<size_t>(handle) * b->S;
   for (int s = 0; s < b->S; ++s)
@@ -715,16 +719,18 @@ rb_status rb_p2p_disconnect_player(rb_p2p* b, int32_t handle, const uint8_t* ses
 }
 
 rb_status rb_p2p_read_status(rb_p2p* b, int32_t* status, int32_t* load_frame, int32_t* n_adv, int32_t* n_save) {
-  std::vector<int32_t> st, tr;
+  std::vector<int32_t> st, tr, cur;
   rb_status r = read_rows(b, b->status, 1, st);
-  if (r == RB_OK) r = read_rows(b, b->trace, TR_COUNT, tr);
+  if (r == RB_OK) r = read_rows(b, b->trace, 1, tr);
+  if (r == RB_OK) r = read_rows(b, b->qs + QS_CUR * b->Spad, 1, cur);
   if (r != RB_OK) return r;
-  const size_t Sp = b->Spad;
-  for (int s = 0; s < b->S; ++s) {
+  for (int s = 0; s < b->S; ++s) {  // trace_pack
+    const uint32_t t = static_cast<uint32_t>(tr[s]);
+    const int32_t na = static_cast<int32_t>((t >> 16) & 0xFFu), ns = static_cast<int32_t>(t >> 24);
     if (status) status[s] = st[s] == kP2PStatusPanic ? RB_PANIC : st[s];
-    if (load_frame) load_frame[s] = tr[TR_LOAD * Sp + s];
-    if (n_adv) n_adv[s] = tr[TR_NADV * Sp + s];
-    if (n_save) n_save[s] = tr[TR_NSAVE * Sp + s];
+    if (load_frame) load_frame[s] = fd_dec(t, cur[s]);
+    if (n_adv) n_adv[s] = na == 0xFF ? -1 : na;
+    if (n_save) n_save[s] = ns == 0xFF ? -1 : ns;
   }
   return RB_OK;
 }
@@ -735,7 +741,11 @@ rb_status rb_p2p_read_frames(rb_p2p* b, int32_t* current, int32_t* confirmed) {
   if (r != RB_OK) return r;
   for (int s = 0; s < b->S; ++s) {
     if (current) current[s] = qs[QS_CUR * b->Spad + s];
-    if (confirmed) confirmed[s] = qs[QS_LAST_CONF * b->Spad + s];
+    if (confirmed) {
+      const size_t Sp = b->Spad;
+      const uint32_t sc = static_cast<uint32_t>(qs[QS_SAVED_CONF * Sp + s]);
+      confirmed[s] = sc == kQsEscWord ? qs[QS_ABS_CONF * Sp + s] : fd_dec(sc >> 16, qs[QS_CUR * Sp + s]);
+    }
   }
   return RB_OK;
 }
@@ -744,12 +754,19 @@ rb_status rb_p2p_read_queues(rb_p2p* b, int32_t* out) {
   std::vector<int32_t> qs;
   rb_status r = read_rows(b, b->qs, kQsFields, qs);
   if (r != RB_OK) return r;
-  static constexpr int kField[RB_P2P_QUEUE_FIELDS] = {QF_LAST_ADDED, QF_TAIL, QF_LEN, QF_LAST_REQ,
-                                                      QF_PRED_FRAME, QF_FIRST_INC, QF_CONN_LAST, QF_DISC};
+  static_assert(RB_P2P_QUEUE_FIELDS == 8, "last added, tail, length, last requested, prediction, first incorrect, connection, disconnected");
+  const size_t Sp = b->Spad;
   for (int s = 0; s < b->S; ++s)
-    for (int h = 0; h < b->P; ++h)
-      for (int k = 0; k < RB_P2P_QUEUE_FIELDS; ++k)
-        out[(static_cast<size_t>(s) * b->P + h) * RB_P2P_QUEUE_FIELDS + k] = qs[(QS_PLAYER0 + kField[k] * 4 + h) * b->Spad + s];
+    for (int h = 0; h < b->P; ++h) {
+      auto row = [&](int field) { return qs[(QS_PLAYER0 + field * 4 + h) * Sp + s]; };
+      uint32_t w[4];
+      int32_t ab[7];
+      for (int i = 0; i < 4; ++i) w[i] = static_cast<uint32_t>(row(QF_LA_CONN + i));
+      for (int i = 0; i < 7; ++i) ab[i] = row(QF_ABS0 + i);
+      const QFields f = q_unpack(w, qs[QS_CUR * Sp + s], ab);
+      const int32_t v[RB_P2P_QUEUE_FIELDS] = {f.la, f.tail, f.len, f.req, f.pred, f.fi, f.conn, f.disc ? 1 : 0};
+      for (int k = 0; k < RB_P2P_QUEUE_FIELDS; ++k) out[(static_cast<size_t>(s) * b->P + h) * RB_P2P_QUEUE_FIELDS + k] = v[k];
+    }
   return RB_OK;
 }
 

@@ -55,7 +55,8 @@
 #endif
 
 /* ABI of the plugin entry points (rb_plugin_abi); bump when the engine's
- * kernel parameter structs change. */
-#define RB_PLUGIN_ABI 6
+ * kernel parameter structs or the layout of the state they point to change
+ * (7: the packed P2P bookkeeping rows). */
+#define RB_PLUGIN_ABI 7
 
 #endif /* GGRS_AMD_GAME_HPP */

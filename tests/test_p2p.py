@@ -642,6 +642,45 @@ def test_gpu_p2p_disconnects_between_fused_launches(gpu_available, monkeypatch, 
 
 
 @pytest.mark.gpu
+def test_gpu_p2p_long_disconnect_takes_the_absolute_rows(gpu_available):
+    """The bookkeeping rows hold frames as 16-bit deltas from the current frame (p2p.hpp q_pack).  A
+    player disconnected for more than 32,767 frames keeps its last added, connection and tail frames,
+    so its rows take the escape bit and the absolute rows.  Statuses, request counts, queues, cells and
+    states equal the oracle's before and after the crossing, through fused lane-asynchronous, kQ and
+    one-tick launches."""
+    import torch
+    P, W, d, rd, mask = 2, 8, 1, 1, 0b01
+    S, T = 70, 32900
+    inputs, upto, rin = synth_network(S, P, T, mask, rd, 1, 5)
+    sess, orc = gpu_pair(G.Game.EX_GAME, S, P, W, d, rd, mask, False)
+    half = np.arange(S) % 2 == 0
+    disc = {30: half, 40: ~half}
+    r1 = np.ascontiguousarray(rin[:64, 1, :])  # the remote frames delivered before the disconnects
+    di, du, dr = (torch.from_numpy(a).cuda() for a in (inputs, upto, rin))
+    cuts = [0, 30] + list(range(31, 42)) + list(range(100, 32750, 50)) + list(range(32750, 32830)) + \
+        list(range(32830, 32878, 8)) + [T]  # one-tick launches across the crossing (cur - 32,767 ~ 32,800)
+    ot = 0
+    for t0, t1 in zip(cuts[:-1], cuts[1:]):
+        if t0 in disc:
+            sess.disconnect_player(1, disc[t0])
+            assert orc.disconnect_player(1, disc[t0]) == 0
+        sess.run_ticks(di[t0:t1], du[t0:t1], dr)
+        for t in range(ot, t1):
+            if t <= 40:  # (a disconnected player's deliveries are ignored, p2p_session.rs:852)
+                assert orc.deliver(1, upto[t, 1], r1) == 0
+            assert orc.add_local_input(0, inputs[t, 0]) == 0
+            res = orc.advance()
+        ot = t1
+        if t1 in (30, 41, 32750, 32790, 32800, 32810, 32830, T):
+            st, lf, na, ns = sess.status()
+            for a, b, what in zip((st, lf, na, ns), res, ("status", "LoadGameState frame", "AdvanceFrames", "saves")):
+                np.testing.assert_array_equal(a, b, err_msg=f"{what}, tick {t1 - 1}")
+            compare_state(sess, orc, t1 - 1)
+    assert (sess.frames()[0] - sess.read_queues()[:, 1, 0] > 32767).all()  # every session's player 1 escaped
+    assert sess.counters()[2] == 0
+
+
+@pytest.mark.gpu
 def test_gpu_disconnect_at_the_current_frame_asserts_like_reference(gpu_available):
     # The device side of test_oracle_disconnect_at_the_current_frame_asserts_like_reference.
     import torch

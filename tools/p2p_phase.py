@@ -15,7 +15,8 @@ import ggrs_amd as G  # noqa: E402
 from ggrs_amd import _lib  # noqa: E402
 from ggrs_amd.p2p import PlayerType, synth_network  # noqa: E402
 
-S, T, W0 = 65536, 96, 48
+S = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+T, W0 = 96, 48
 inputs, upto, rin = synth_network(S, 2, T, 0b1, 2, 1, 4)
 di, du, dr = (torch.from_numpy(a).cuda() for a in (inputs, upto, rin))
 b = (G.SessionBuilder(G.Game.EX_GAME, num_sessions=S).with_num_players(2).with_max_prediction_window(8)
