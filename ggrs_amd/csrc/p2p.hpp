@@ -741,9 +741,17 @@ __device__ __forceinline__ void q_discard(DevQueue& q, int32_t frame) {
 // AdvanceFrame's input fetch.  Measured (interleaved A/B, profiles/r05_ab_qsel.log): one-tick
 // launches 11.20 -> 10.44 us of wall per tick, 50-tick launches 3.48 -> 3.43 us; with sparse saving
 // 9.70 -> 10.27 us, so the sparse kernels keep the branches.
+// Attribution builds (tools/mkvar.sh -DRB_P2P_EXP=...): 1 drops the game's
+// AdvanceFrame math, 2 its save checksum, 32 returns at entry (the launch
+// floor), 64 drops the trace rows and work counters, 128 the sparse dry run, 256
+// every input-ring read of InputQueue::input.  Always 0 in the product.
+#ifndef RB_P2P_EXP
+#define RB_P2P_EXP 0
+#endif
 template <bool kSel, class R>
 __device__ __forceinline__ uint32_t q_input(DevQueue& q, const R& r, int h, unsigned s, int32_t f) {
   q.last_req = f;
+  if constexpr ((RB_P2P_EXP & 256) != 0) return q.pred_val;  // (attribution builds only: no ring read)
   q.bad |= f < q.tail;  // assert!(requested_frame >= self.inputs[self.tail].frame) (:113)
   if constexpr (kSel) {
     const bool np = q.pred_frame < 0;
@@ -807,12 +815,6 @@ constexpr int kFanGroup = RB_FAN_GROUP;  // chains a lane advances together (ind
 // network-fed bookkeeping (desync detection, peers' connect-status reports)
 // are compiled in only where the batch uses them (fewer live scalars: no SGPR
 // spills on the plain path)
-// Attribution builds (tools/mkvar.sh -DRB_P2P_EXP=...): 1 drops the game's
-// AdvanceFrame math, 2 its save checksum, 32 returns at entry (the launch
-// floor), 64 drops the trace rows and work counters.  Always 0 in the product.
-#ifndef RB_P2P_EXP
-#define RB_P2P_EXP 0
-#endif
 // kAsync (plain path with the LDS snapshot ring only): lane-asynchronous
 // ticks.  Every loop iteration a session executes exactly one AdvanceFrame:
 // a resimulated frame of its current rollback ([SaveGameState], its
@@ -828,6 +830,9 @@ constexpr int kFanGroup = RB_FAN_GROUP;  // chains a lane advances together (ind
 // operations run in the reference's order, except that the tick's final
 // SaveGameState moves behind set_last_confirmed_frame and add_local_input,
 // which touch neither the state nor the cells.
+#ifndef RB_P2P_SHORT_WAVES
+#define RB_P2P_SHORT_WAVES 4  // waves per SIMD the short-launch kernels (kQ, one-tick) are compiled for (A/B builds)
+#endif
 #ifndef RB_P2P_WAVES_PER_EU
 #define RB_P2P_WAVES_PER_EU 1  // >1: ask the compiler for that many waves per SIMD (VGPR cap; A/B builds)
 #endif
@@ -874,7 +879,7 @@ template <class G, bool kSpec, bool kSparse, bool kNet, bool kLdsC, bool kAsync,
 // The launches that keep the cells in HBM on the plain / sparse path (kQ, and the one-tick launches
 // of live play) are capped at 128 VGPRs the same way: four waves per SIMD once a batch has them.
 __global__ void __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu((kQ && kSpec) ? RB_SPEC_Q_WAVES : (kQ || (!kLdsC && !kSpec && !kNet)) ? 4 : RB_P2P_WAVES_PER_EU)))
+__attribute__((amdgpu_waves_per_eu((kQ && kSpec) ? RB_SPEC_Q_WAVES : (kQ || (!kLdsC && !kSpec && !kNet)) ? RB_P2P_SHORT_WAVES : RB_P2P_WAVES_PER_EU)))
 p2p_kernel(const P2PParams p) {
   static_assert(!kAsync || (kLdsC && !kSpec && !kNet), "lane-asynchronous ticks: plain or sparse path, LDS cells");
   static_assert(!kWire || (!kSpec && !kSparse && !kNet && !kAsync), "packet-fed ticks: the plain lock-step path");
@@ -1710,12 +1715,17 @@ p2p_kernel(const P2PParams p) {
   auto tick_begin = [&](int t) __attribute__((always_inline)) -> int {
     const int tn = t + 1 < p.T ? t + 1 : t;
 
+    // A one-tick launch has no next tick to prefetch for (measured: 10.40 -> 9.96 us per one-tick launch
+    // at 65,536 sessions, 94.5 -> 91.6 at 1,048,576; profiles/r06_ab_short_waves.log)
+    const bool pre_next = p.T > 1;
     if constexpr (kPrefetch) {
+      if (pre_next) {
 #pragma unroll
-      for (int j = 0; j < PPL; ++j) {
-        up_n[j] = load_upto(tn, j);
-        lin_n[j] = load_local(tn, j);
-        if constexpr (kWire) pre_n[j] = wire_fetch(min(player_of(j), P - 1), tn);
+        for (int j = 0; j < PPL; ++j) {
+          up_n[j] = load_upto(tn, j);
+          lin_n[j] = load_local(tn, j);
+          if constexpr (kWire) pre_n[j] = wire_fetch(min(player_of(j), P - 1), tn);
+        }
       }
     }
     status = kP2PStatusOk;
@@ -1750,11 +1760,13 @@ p2p_kernel(const P2PParams p) {
       }
     }
     if constexpr (kPrefetch) {
+      if (pre_next) {
 #pragma unroll
-      for (int j = 0; j < PPL; ++j) {
-        const int32_t f = remote_start(j);
+        for (int j = 0; j < PPL; ++j) {
+          const int32_t f = remote_start(j);
 #pragma unroll
-        for (int k = 0; k < kPre; ++k) rv_n[j][k] = load_remote(j, f + k);
+          for (int k = 0; k < kPre; ++k) rv_n[j][k] = load_remote(j, f + k);
+        }
       }
     }
     {  // input_queue.rs:181 assert!(self.length <= INPUT_QUEUE_LENGTH) fired during the poll.  No
