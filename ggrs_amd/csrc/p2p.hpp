@@ -744,7 +744,8 @@ __device__ __forceinline__ void q_discard(DevQueue& q, int32_t frame) {
 // Attribution builds (tools/mkvar.sh -DRB_P2P_EXP=...): 1 drops the game's
 // AdvanceFrame math, 2 its save checksum, 32 returns at entry (the launch
 // floor), 64 drops the trace rows and work counters, 128 the sparse dry run, 256
-// every input-ring read of InputQueue::input.  Always 0 in the product.
+// every input-ring read of InputQueue::input (and with it every prediction, so no
+// session rolls back: the rollback work).  Always 0 in the product.
 #ifndef RB_P2P_EXP
 #define RB_P2P_EXP 0
 #endif
