@@ -1717,8 +1717,11 @@ p2p_kernel(const P2PParams p) {
     const int tn = t + 1 < p.T ? t + 1 : t;
 
     // A one-tick launch has no next tick to prefetch for (measured: 10.40 -> 9.96 us per one-tick launch
-    // at 65,536 sessions, 94.5 -> 91.6 at 1,048,576; profiles/r06_ab_short_waves.log)
-    const bool pre_next = p.T > 1;
+    // at 65,536 sessions, 94.5 -> 91.6 at 1,048,576; profiles/r06_ab_short_waves.log).  The packet-fed
+    // fused launches (kWire with the LDS ring) prefetch without the branch: with it their ticks ran
+    // 4.88 -> 5.26 us, while the plain fused ticks run faster with it (3.37 -> 3.11 us; sparse and the
+    // C4 fan-out neutral; profiles/r06_ab_prefetch_branch.log).
+    const bool pre_next = (kWire && kLdsC) || p.T > 1;
     if constexpr (kPrefetch) {
       if (pre_next) {
 #pragma unroll
