@@ -74,7 +74,7 @@ LINES = {
                f"{Q4} S=65536 fanout", 50),
     "c4_k8": (f"{P2P} --num-players 4 --fanout --fanout-k 8 --steps 100 --warmup 50",
               f"{P2P} --num-players 4 --fanout --fanout-k 8 --steps 100 --warmup 50", f"{Q4} S=65536 fanout8", 50),
-    "brawler_fan": (f"--game brawler {P2P} --fanout --steps 20 --warmup 100 --ticks-per-launch 20",
+    "brawler_fan": (f"--game brawler {P2P} --fanout --steps 60 --warmup 100 --ticks-per-launch 20",
                     f"--game brawler {P2P} --fanout --steps 20 --warmup 80", f"{QB} S=65536 fanout tpl=20", 20),
     "wire": (f"{P2P} --wire --steps 200 --warmup 32", f"{P2P} --wire --steps 100 --warmup 16", f"{Q} S=65536 wire tpl=1", 1),
     "wire_replay": (f"{P2P} --wire-replay --steps 400 --warmup 50", f"{P2P} --wire-replay --steps 200 --warmup 50",
