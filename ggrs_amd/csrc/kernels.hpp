@@ -1047,6 +1047,13 @@ struct GameOpsT final : GameOps {
         return rb_launch(k, dim3(grid), dim3(block), static_cast<uint32_t>(lds), st, ev, p);
       }
     }
+    // live play, one tick per launch: the tick count compiled in (p2p_kernel kOne: 121 -> 99 VGPRs, no
+    // SGPR spills; 9.70 -> 9.59 us at 65,536 sessions, packet-fed 11.07 -> 10.45; r06_ab_one_tick.log)
+    if constexpr (!kSpec && !kNet) {
+      if (p.T == 1)
+        return rb_launch(p2p_kernel<G, kSpec, kSparse, kNet, false, false, false, kMtf, false, true>, dim3(grid),
+                         dim3(block), static_cast<uint32_t>(lds), st, ev, p);
+    }
     return rb_launch(p2p_kernel<G, kSpec, kSparse, kNet, false, false, false, kMtf>, dim3(grid), dim3(block),
                      static_cast<uint32_t>(lds), st, ev, p);
   }
@@ -1076,6 +1083,9 @@ struct GameOpsT final : GameOps {
           return rb_launch(k, dim3(grid), dim3(block), static_cast<uint32_t>(lds), st, ev, p);
         }
       }
+      if (p.T == 1)  // one tick per launch (kOne, above)
+        return rb_launch(p2p_kernel<G, false, false, false, false, false, true, false, false, true>, dim3(grid),
+                         dim3(block), static_cast<uint32_t>(lds), st, ev, p);
       return rb_launch(p2p_kernel<G, false, false, false, false, false, true>, dim3(grid), dim3(block),
                        static_cast<uint32_t>(lds), st, ev, p);
     }

@@ -831,6 +831,9 @@ constexpr int kFanGroup = RB_FAN_GROUP;  // chains a lane advances together (ind
 // operations run in the reference's order, except that the tick's final
 // SaveGameState moves behind set_last_confirmed_frame and add_local_input,
 // which touch neither the state nor the cells.
+#ifndef RB_P2P_ONE_WAVES
+#define RB_P2P_ONE_WAVES 4  // waves per SIMD the one-tick kernels (kOne) are compiled for
+#endif
 #ifndef RB_P2P_SHORT_WAVES
 #define RB_P2P_SHORT_WAVES 4  // waves per SIMD the short-launch kernels (kQ, one-tick) are compiled for (A/B builds)
 #endif
@@ -873,14 +876,14 @@ __device__ uint64_t rb_p2p_phase[8 * 4096];
   } while (0)
 #endif
 template <class G, bool kSpec, bool kSparse, bool kNet, bool kLdsC, bool kAsync, bool kWire = false, bool kMtf = false,
-          bool kQ = false>
+          bool kQ = false, bool kOne = false>
 // kQ (the input ring alone in LDS, 32 KiB per 256 threads) is capped at 128 VGPRs: with the cells in
 // HBM four workgroups fit a CU, so batches of more than two waves per SIMD run four resident instead
 // of the LDS-cell kernel's two (kernels.hpp launch_p2p_as_m).
 // The launches that keep the cells in HBM on the plain / sparse path (kQ, and the one-tick launches
 // of live play) are capped at 128 VGPRs the same way: four waves per SIMD once a batch has them.
 __global__ void __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu((kQ && kSpec) ? RB_SPEC_Q_WAVES : (kQ || (!kLdsC && !kSpec && !kNet)) ? RB_P2P_SHORT_WAVES : RB_P2P_WAVES_PER_EU)))
+__attribute__((amdgpu_waves_per_eu(kOne ? RB_P2P_ONE_WAVES : (kQ && kSpec) ? RB_SPEC_Q_WAVES : (kQ || (!kLdsC && !kSpec && !kNet)) ? RB_P2P_SHORT_WAVES : RB_P2P_WAVES_PER_EU)))
 p2p_kernel(const P2PParams p) {
   static_assert(!kAsync || (kLdsC && !kSpec && !kNet), "lane-asynchronous ticks: plain or sparse path, LDS cells");
   static_assert(!kWire || (!kSpec && !kSparse && !kNet && !kAsync), "packet-fed ticks: the plain lock-step path");
@@ -895,6 +898,10 @@ p2p_kernel(const P2PParams p) {
   const unsigned s = g / L;
   const int lane = static_cast<int>(g % L);
   const bool lead = lane == 0;
+  // kOne: the launches of one tick (live play), the tick count a compile-time 1, so the tick loop
+  // and the next tick's prefetch compile away (kernels.hpp launch_p2p_as_m)
+  static_assert(!kOne || (!kLdsC && !kAsync && !kQ), "one-tick launches keep the cells in HBM");
+  const int T = kOne ? 1 : p.T;
   if (p.launch_clock) launch_clock_put(p.launch_clock, g / 64u, 0u);
   if (s >= static_cast<unsigned>(p.S)) return;  // whole lane groups leave together
 #if RB_P2P_PHASE
@@ -1714,14 +1721,14 @@ p2p_kernel(const P2PParams p) {
   // 2 = rollback_and_save, add_local_input and the new frame follow.
   // (the next tick's deliveries are prefetched unless kPrefetch is false, above)
   auto tick_begin = [&](int t) __attribute__((always_inline)) -> int {
-    const int tn = t + 1 < p.T ? t + 1 : t;
+    const int tn = t + 1 < T ? t + 1 : t;
 
     // A one-tick launch has no next tick to prefetch for (measured: 10.40 -> 9.96 us per one-tick launch
     // at 65,536 sessions, 94.5 -> 91.6 at 1,048,576; profiles/r06_ab_short_waves.log).  The packet-fed
     // fused launches (kWire with the LDS ring) prefetch without the branch: with it their ticks ran
     // 4.88 -> 5.26 us, while the plain fused ticks run faster with it (3.37 -> 3.11 us; sparse and the
     // C4 fan-out neutral; profiles/r06_ab_prefetch_branch.log).
-    const bool pre_next = (kWire && kLdsC) || p.T > 1;
+    const bool pre_next = (kWire && kLdsC) || T > 1;
     if constexpr (kPrefetch) {
       if (pre_next) {
 #pragma unroll
@@ -2344,9 +2351,9 @@ p2p_kernel(const P2PParams p) {
                                                 // better than the rotation at 4 waves per SIMD here)
 #endif
   if constexpr (!kAsync) {
-    for (int t = 0; t < p.T; ++t) {
+    for (int t = 0; t < T; ++t) {
 #if RB_P2P_PRIO
-      if (p.T > 1) prio_turn(wslot);
+      if (T > 1) prio_turn(wslot);
 #endif
       if (!tick(t)) break;
     }
